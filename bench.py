@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the batched FFMP step on MI355X (driver contract).
+
+One "step" = one FFMPVec step of every env this rank owns: the env kernel
+(integrate, obstacles, lidar, collision/reward/done, auto-reset) + the raster
+kernel (both float32 frames of state_m and the float32 potential plane).
+Actions for every timed step are pre-generated on the device (inputs resident
+in HBM before the timed region).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+N=1 workload: BASELINE config C3 (32,768 envs, 256x256 grid, 16 moving discs,
+180-beam lidar) — the largest single-GPU config and the one the north-star
+target (256x256, 32k envs) is quoted on.  For N>1 each rank owns its own C3
+batch (weak scaling, no data-path collective); C4/C5 (--config) split their
+total env count over the ranks (strong scaling).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (batched gym_ffmp) at 1/2/4/8 MI355X; HBM-roofline %"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
+    p.add_argument("--envs", type=int, default=0, help="override envs per rank")
+    p.add_argument("--no-potential", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds: float):
+    """The NumPy oracle (oracle/ffmp_oracle.py) stepping a bounded sample of the same workload."""
+    import numpy as np
+    from oracle.ffmp_oracle import OracleVecEnv
+    n = 4
+    env = OracleVecEnv(cfg, n)
+    env.reset()
+    rng = np.random.default_rng(0)
+    env.step(rng.integers(0, 28, n))  # warm
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        env.step(rng.integers(0, 28, n))
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} envs x {steps} steps of the same config ({el:.1f} s), NumPy oracle "
+                      f"OracleVecEnv, 1 process / 1 thread"}
+
+
+def load_traffic(workload: str, n_envs: int):
+    """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if int(d.get("n_envs", -1)) != n_envs:
+            return None
+        return float(d["raster_hbm_bytes_per_launch"])
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from flow_field_based_motion_planner_amd.config import PRESETS, bytes_per_env_step, preset
+    from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    name = args.config
+    pr = PRESETS[name]
+    cfg = preset(name, seed=args.seed)
+    strong = pr["gpus"] > 1
+    n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
+    n_total = n * world
+    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential)
+
+    K, W = args.steps, args.warmup
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
+    env.reset()
+    for w in range(W):
+        env.step_state(actions[w])
+        env.raster()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+            torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        e0, e1, e2 = evs[k]
+        e0.record()
+        env.step_state(actions[W + k])
+        e1.record()
+        env.raster()
+        e2.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    env.check_errors()
+
+    raster_ms = sum(evs[k][1].elapsed_time(evs[k][2]) for k in range(K)) / K
+    state_ms = sum(evs[k][0].elapsed_time(evs[k][1]) for k in range(K)) / K
+    b = bytes_per_env_step(cfg, potential=not args.no_potential)
+    achieved = b["raster"] * n / (raster_ms * 1e-3) / 1e9
+    traffic = load_traffic(name, n)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": n_total * K / el,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": el * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
+                       "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
+                       "potential": not args.no_potential, "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": traffic,
+                         "kernel": "raster_kernel", "kernel_ms": raster_ms,
+                         "algorithmic_bytes_per_launch": b["raster"] * n},
+            "env_kernel_ms": state_ms,
+            "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,256 @@
+// ffmp_device.h — device-side building blocks of the batched FFMP step.
+//
+// Arithmetic contract (mirrored operation-for-operation by oracle/ffmp_oracle.py;
+// compile with -ffp-contract=off so no a*b+c is fused):
+//   * per-env scalars (pose, goal, obstacles, lidar, reward) in float64, like
+//     the reference's Python floats (src/train.py:167-188, ffmp.py:130-157);
+//   * per-cell raster maths in float32 (the BEV planes are float32 tensors,
+//     src/train.py:116-121, :543-545).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/ffmp.h"
+
+#pragma clang fp contract(off)
+
+#define FFMP_DEV __device__ __forceinline__
+
+namespace ffmp {
+
+constexpr double kPi = 3.141592653589793;       // math.pi
+constexpr double kTwoPi = 2.0 * 3.141592653589793;  // 2 * math.pi (train.py:169)
+constexpr double kInv2p32 = 2.3283064365386962890625e-10;  // 2^-32
+
+// RobotAction.cmd (src/gym_ffmp/envs/robot/config.py:28-55): id = 7*vi + wi.
+// Stored as the literal lists, never computed (0.6 != 3*0.2 in binary).
+__constant__ double kCmdV[4] = {0.0, 0.2, 0.4, 0.6};
+__constant__ double kCmdW[7] = {-0.6, -0.4, -0.2, 0.0, 0.2, 0.4, 0.6};
+
+// ROSNode.pi_to_pi (src/train.py:167-172): iterative wrap into (-pi, pi].
+// (+-inf would loop forever in the reference; returned unchanged here.)
+FFMP_DEV double pi_to_pi(double a) {
+  if (!(a - a == 0.0)) return a;  // inf / nan
+  while (a >= kPi) a = a - kTwoPi;
+  while (a <= -kPi) a = a + kTwoPi;
+  return a;
+}
+
+// ---------------- Philox4x32-10 (Salmon et al., SC'11) ----------------------
+struct U4 { uint32_t x, y, z, w; };
+
+FFMP_DEV U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                          uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+// counter = (draw index, episode, global env lo, global env hi), key = seed.
+FFMP_DEV U4 draw(const ffmp_cfg_t& cfg, int64_t genv, int32_t episode, uint32_t idx) {
+  const uint64_t g = (uint64_t)genv;
+  return philox4x32_10(idx, (uint32_t)episode, (uint32_t)g, (uint32_t)(g >> 32),
+                       (uint32_t)cfg.seed, (uint32_t)(cfg.seed >> 32));
+}
+FFMP_DEV double u01(uint32_t r) { return (double)r * kInv2p32; }
+
+// Draw-index layout of one episode's reset.
+constexpr uint32_t kDrawObst = 1;                       // + k*16 + try
+constexpr int kObstTries = 16;
+constexpr uint32_t kDrawVel = 1 + FFMP_MAX_OBST * kObstTries;  // + k
+
+// ---------------- per-env episode sampling ----------------------------------
+struct Episode {
+  double x, y, yaw, gx, gy;
+};
+
+FFMP_DEV Episode sample_episode(const ffmp_cfg_t& cfg, int64_t genv, int32_t episode) {
+  const U4 b = draw(cfg, genv, episode, 0);
+  Episode ep;
+  ep.x = 0.0;
+  ep.y = 0.0;
+  ep.yaw = u01(b.x) * kTwoPi - kPi;
+  const double gd = cfg.goal_min + u01(b.y) * (cfg.goal_max - cfg.goal_min);
+  const double gb = u01(b.z) * kTwoPi - kPi;
+  ep.gx = gd * cos(gb);
+  ep.gy = gd * sin(gb);
+  return ep;
+}
+
+struct Obst {
+  double x, y, vx, vy, r;
+};
+
+FFMP_DEV Obst sample_obstacle(const ffmp_cfg_t& cfg, int64_t genv, int32_t episode, int k,
+                              const Episode& ep) {
+  const double W = cfg.world_half;
+  Obst o;
+  bool ok = false;
+  for (int tr = 0; tr < kObstTries && !ok; ++tr) {
+    const U4 b = draw(cfg, genv, episode, kDrawObst + (uint32_t)(k * kObstTries + tr));
+    o.r = cfg.obst_rmin + u01(b.z) * (cfg.obst_rmax - cfg.obst_rmin);
+    const double span = 2.0 * (W - o.r);
+    o.x = (o.r - W) + u01(b.x) * span;
+    o.y = (o.r - W) + u01(b.y) * span;
+    const double ds = o.r + cfg.start_clear, dg = o.r + cfg.goal_clear;
+    const double sx = o.x - ep.x, sy = o.y - ep.y;
+    const double gx = o.x - ep.gx, gy = o.y - ep.gy;
+    ok = (sx * sx + sy * sy > ds * ds) && (gx * gx + gy * gy > dg * dg);
+  }
+  o.vx = 0.0;
+  o.vy = 0.0;
+  if (!ok) {  // parked: zero radius far outside the world
+    o.x = 3.0 * W;
+    o.y = 3.0 * W;
+    o.r = 0.0;
+  } else if (cfg.moving) {
+    const U4 b = draw(cfg, genv, episode, kDrawVel + (uint32_t)k);
+    const double sp = u01(b.x) * cfg.obst_vmax;
+    const double hd = u01(b.y) * kTwoPi - kPi;
+    o.vx = sp * cos(hd);
+    o.vy = sp * sin(hd);
+  }
+  return o;
+}
+
+// Obstacle motion with specular reflection off the world walls; parked discs
+// (r == 0) stay where they are.
+FFMP_DEV void move_obstacle(const ffmp_cfg_t& cfg, Obst& o) {
+  if (!(o.r > 0.0)) return;
+  const double W = cfg.world_half;
+  o.x = o.x + o.vx * cfg.dt;
+  if (o.x > W - o.r) { o.x = 2.0 * (W - o.r) - o.x; o.vx = -o.vx; }
+  else if (o.x < o.r - W) { o.x = 2.0 * (o.r - W) - o.x; o.vx = -o.vx; }
+  o.y = o.y + o.vy * cfg.dt;
+  if (o.y > W - o.r) { o.y = 2.0 * (W - o.r) - o.y; o.vy = -o.vy; }
+  else if (o.y < o.r - W) { o.y = 2.0 * (o.r - W) - o.y; o.vy = -o.vy; }
+}
+
+// ---------------- raster record (per env, float32) ---------------------------
+// hdr[0..3] current frame {px, py, cos yaw, sin yaw}; hdr[4..7] previous frame;
+// hdr[8..9] goal in the current ego frame; then K float4 {ox, oy, r*r, r} of the
+// current frame in ego coordinates, then K float4 of the previous frame.
+struct FrameHdr {
+  float px, py, c, s;
+};
+
+FFMP_DEV FrameHdr make_hdr(double x, double y, double c, double s) {
+  return FrameHdr{(float)x, (float)y, (float)c, (float)s};
+}
+
+// World point -> ego frame (float64), rounded to float32.
+FFMP_DEV float2 to_ego(double wx, double wy, double x, double y, double c, double s) {
+  const double rx = wx - x, ry = wy - y;
+  const double ex = c * rx + s * ry;
+  const double ey = c * ry - s * rx;
+  return make_float2((float)ex, (float)ey);
+}
+
+FFMP_DEV float4 ego_obst(const Obst& o, double x, double y, double c, double s) {
+  const float2 e = to_ego(o.x, o.y, x, y, c, s);
+  const float rf = (float)o.r;
+  return make_float4(e.x, e.y, rf * rf, rf);
+}
+
+// Ego coordinate of cell index i (row -> ego x, col -> ego y): reference's
+// `i * map_grid_size - 0.5 * map_range` (ffmp.py:89-90) in float32.
+FFMP_DEV float cell_coord(const ffmp_cfg_t& cfg, int i) {
+  return (float)i * cfg.res_f - cfg.half_f;
+}
+
+// Outside-the-world test of an ego point (float32).
+FFMP_DEV bool outside_world(const ffmp_cfg_t& cfg, const FrameHdr& h, float ex, float ey) {
+  const float wx = h.px + (h.c * ex - h.s * ey);
+  const float wy = h.py + (h.s * ex + h.c * ey);
+  const float W = cfg.world_half_f;
+  return (wx < -W) | (wx > W) | (wy < -W) | (wy > W);
+}
+
+FFMP_DEV bool in_disc(float ex, float ey, const float4& o) {
+  const float dx = ex - o.x, dy = ey - o.y;
+  return dx * dx + dy * dy <= o.z;
+}
+
+// Repulsive term of one obstacle at an ego point; returns 0 contribution flag.
+FFMP_DEV float add_repulsive(const ffmp_cfg_t& cfg, float U, float ex, float ey, const float4& o) {
+  const float dx = ex - o.x, dy = ey - o.y;
+  float d = sqrtf(dx * dx + dy * dy) - o.w;
+  d = fmaxf(d, cfg.rho_min_f);
+  if (d < cfg.rho0_f) {
+    const float q = 1.0f / d - cfg.inv_rho0_f;
+    U = U + cfg.half_kr_f * (q * q);
+  }
+  return U;
+}
+
+FFMP_DEV float attractive(const ffmp_cfg_t& cfg, float ex, float ey, float gx, float gy) {
+  const float dx = ex - gx, dy = ey - gy;
+  return cfg.half_ka_f * (dx * dx + dy * dy);
+}
+
+// Full (unculled) potential at cell (i, j) — used for the gradient lookup.
+FFMP_DEV float potential_cell(const ffmp_cfg_t& cfg, const float4* obs, int K, float gx, float gy,
+                              int i, int j) {
+  const float ex = cell_coord(cfg, i), ey = cell_coord(cfg, j);
+  float U = attractive(cfg, ex, ey, gx, gy);
+  for (int k = 0; k < K; ++k) U = add_repulsive(cfg, U, ex, ey, obs[k]);
+  return U;
+}
+
+FFMP_DEV bool occupied_cell(const ffmp_cfg_t& cfg, const FrameHdr& h, const float4* obs, int K,
+                            int i, int j) {
+  const float ex = cell_coord(cfg, i), ey = cell_coord(cfg, j);
+  bool o = outside_world(cfg, h, ex, ey);
+  for (int k = 0; k < K; ++k) o |= in_disc(ex, ey, obs[k]);
+  return o;
+}
+
+// One lidar beam (float64): nearest of the K discs and the 4 world walls.
+// Returns +inf for no return within lidar_max, -inf if the origin is inside a disc.
+FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, double x, double y, double c, double s,
+                           double bc, double bs, const double* ox, const double* oy,
+                           const double* orad, int K) {
+  const double dirx = c * bc - s * bs;
+  const double diry = s * bc + c * bs;
+  const double inf = __builtin_inf();
+  double best = inf;
+  bool inside = false;
+  for (int k = 0; k < K; ++k) {
+    const double rx = ox[k] - x, ry = oy[k] - y;
+    const double rr = rx * rx + ry * ry;
+    const double r2 = orad[k] * orad[k];
+    inside |= rr <= r2;
+    const double tp = rx * dirx + ry * diry;
+    if (tp > 0.0) {
+      const double perp = rr - tp * tp;
+      if (perp <= r2) {
+        const double h = tp - sqrt(r2 - perp);
+        if (h <= cfg.lidar_max && h < best) best = h;
+      }
+    }
+  }
+  const double W = cfg.world_half;
+  if (dirx > 0.0) { const double h = (W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; }
+  else if (dirx < 0.0) { const double h = (-W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; }
+  if (diry > 0.0) { const double h = (W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; }
+  else if (diry < 0.0) { const double h = (-W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; }
+  return inside ? -inf : best;
+}
+
+// FFMP.is_collision2 on one float32 beam (ffmp.py:110-115): `if r:` skips 0,
+// `r < ROBOT_RSIZE` is a float64 compare.
+FFMP_DEV bool beam_collides(float r, double thr) { return (r != 0.0f) && ((double)r < thr); }
+
+// FFMP.reward_calculator (ffmp.py:130-157), float64, (r_g + r_c) + r_s.
+FFMP_DEV double reward_calc(double dist, double d0, bool col, bool goal) {
+  const double r_g = goal ? 1.0 : 0.05 * (d0 - dist);
+  const double r_c = col ? -1.0 : 0.0;
+  return (r_g + r_c) + (-0.05);
+}
+
+}  // namespace ffmp

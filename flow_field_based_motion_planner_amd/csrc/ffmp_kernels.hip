@@ -1,0 +1,659 @@
+// ffmp_kernels.hip — CDNA4 (gfx950) kernels + C ABI of libffmp.
+//
+// Kernels
+//   env_kernel<MODE>   one 64-lane wave per env: action -> unicycle integrate,
+//                      obstacle motion, lidar (lane per beam), footprint
+//                      collision (lane per footprint cell), goal/reward/done,
+//                      truncation, auto-reset (Philox), gradient lookup, and the
+//                      per-env raster record. Tiny per env; latency-hidden.
+//   raster_kernel      the HBM-bound hot kernel: 256 threads x 4 cells per pass,
+//                      writes the two float32 occupancy frames of state_m and
+//                      the float32 potential plane with 16-B stores; obstacles
+//                      staged in LDS and culled per 256-cell wave chunk.
+//   reward_done_kernel / footprint_kernel / scan_kernel — legacy FFMP methods.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <stddef.h>
+#include <string.h>
+
+#include "ffmp_device.h"
+
+#pragma clang fp contract(off)
+
+using namespace ffmp;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+__attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: HIP launch failed: %s", what, hipGetErrorString(e));
+    return FFMP_E_HIP;
+  }
+  return FFMP_OK;
+}
+
+int check_cfg(const ffmp_cfg_t* c) {
+  if (!c) return fail(FFMP_E_ARG, "cfg is NULL");
+  if (c->grid < 8 || c->grid > 4096 || (c->grid % 4) != 0)
+    return fail(FFMP_E_CFG, "grid must be a multiple of 4 in [8,4096], got %d", c->grid);
+  if (c->n_obst < 0 || c->n_obst > FFMP_MAX_OBST)
+    return fail(FFMP_E_CFG, "n_obst out of range: %d", c->n_obst);
+  if (c->n_beams < 0 || c->n_beams > FFMP_MAX_BEAMS)
+    return fail(FFMP_E_CFG, "n_beams out of range: %d", c->n_beams);
+  if (c->n_foot < 0 || c->n_foot > FFMP_MAX_FOOT)
+    return fail(FFMP_E_CFG, "n_foot out of range: %d", c->n_foot);
+  if (c->n_beams > 0 && !c->beam_cs) return fail(FFMP_E_CFG, "beam_cs is NULL with n_beams > 0");
+  for (int f = 0; f < c->n_foot; ++f) {
+    const int i = c->grid / 2 + c->foot_di[f], j = c->grid / 2 + c->foot_dj[f];
+    if (i < 0 || j < 0 || i >= c->grid || j >= c->grid)
+      return fail(FFMP_E_CFG, "footprint cell outside the grid (index %d)", f);
+  }
+  return FFMP_OK;
+}
+
+constexpr int kEnvMode_Step = 0;
+constexpr int kEnvMode_Reset = 1;
+
+__host__ __device__ inline int64_t rec_stride(int K) { return FFMP_REC_HDR + 8 * (int64_t)K; }
+
+}  // namespace
+
+// ============================================================================
+// env_kernel: one wave (64 lanes) = one env.
+// ============================================================================
+template <int MODE>
+__global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+                                                 const int64_t* __restrict__ action,
+                                                 const uint8_t* __restrict__ mask, int32_t initial,
+                                                 ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
+  __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST];
+  __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
+
+  const int64_t e = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (e >= n) return;
+  if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
+
+  const int K = cfg.n_obst;
+  const int L = cfg.n_beams;
+  const int G = cfg.grid;
+  const int ic = G / 2;
+  const int64_t genv = env_offset + e;
+
+  // ---- load (uniform scalars in every lane; obstacle k in lane k) ----
+  double x0 = st.pose[e * 3 + 0], y0 = st.pose[e * 3 + 1], yaw0 = st.pose[e * 3 + 2];
+  double gx = st.goal[e * 2 + 0], gy = st.goal[e * 2 + 1];
+  double d0 = st.d0[e];
+  int32_t t = st.t[e];
+  int32_t episode = st.episode[e];
+  Obst my{0.0, 0.0, 0.0, 0.0, 0.0};
+  const bool has_obst = lane < K;
+  if (MODE == kEnvMode_Step && has_obst) {
+    const double* p = st.obst + (e * K + lane) * 4;
+    my.x = p[0]; my.y = p[1]; my.vx = p[2]; my.vy = p[3];
+    my.r = st.obst_r[e * K + lane];
+  }
+
+  double x1 = x0, y1 = y0, yaw1 = yaw0;
+  double c0 = 0.0, s0 = 0.0;
+  double vlin = 0.0, vang = 0.0;
+  float t_obs = 0.0f;
+  bool col = false, goal = false, trunc = false, done = false;
+  double reward = 0.0;
+  bool reset_now = (MODE == kEnvMode_Reset);
+
+  if (MODE == kEnvMode_Step) {
+    // ---- action -> (v, w) (train.py:668-673 -> Gazebo /cmd_vel) ----
+    int64_t a = action[e];
+    if (a < 0 || a >= FFMP_N_ACTIONS) {
+      if (lane == 0) atomicOr(st.err, 1u);
+      a = 3;  // (0.0, 0.0)
+    }
+    const double v = kCmdV[a / 7], w = kCmdW[a % 7];
+    // ---- unicycle integrator (SPEC a15) ----
+    c0 = cos(yaw0);
+    s0 = sin(yaw0);
+    x1 = x0 + (v * c0) * cfg.dt;
+    y1 = y0 + (v * s0) * cfg.dt;
+    yaw1 = pi_to_pi(yaw0 + w * cfg.dt);
+    // previous frame record from the pre-step pose / obstacle positions
+    if (has_obst) {
+      s_eprev[lane] = ego_obst(my, x0, y0, c0, s0);
+      if (cfg.moving) move_obstacle(cfg, my);
+    }
+    t = t + 1;
+    // ---- velocity (train.py:182-188): per-step displacement ----
+    const double ddx = x1 - x0, ddy = y1 - y0;
+    vlin = sqrt(ddx * ddx + ddy * ddy);
+    vang = pi_to_pi(yaw1 - yaw0);
+    t_obs = (float)cfg.dt;
+  }
+
+  if (has_obst) { s_ox[lane] = my.x; s_oy[lane] = my.y; s_or[lane] = my.r; }
+  double c1 = cos(yaw1), s1 = sin(yaw1);
+  if (has_obst) s_ecur[lane] = ego_obst(my, x1, y1, c1, s1);
+  __syncthreads();
+
+  FrameHdr hcur = make_hdr(x1, y1, c1, s1);
+  FrameHdr hprev = (MODE == kEnvMode_Step) ? make_hdr(x0, y0, c0, s0) : hcur;
+
+  if (MODE == kEnvMode_Step) {
+    // ---- relative goal (train.py:174-180) ----
+    const double dx = gx - x1, dy = gy - y1;
+    const double dist = sqrt(dx * dx + dy * dy);
+    // ---- collision: footprint on the current occupancy (ffmp.py:85-105) ----
+    bool c_foot = false;
+    if (cfg.collide_mode & FFMP_COLLIDE_FOOTPRINT) {
+      for (int f = lane; f < cfg.n_foot; f += 64)
+        c_foot |= occupied_cell(cfg, hcur, s_ecur, K, ic + cfg.foot_di[f], ic + cfg.foot_dj[f]);
+    }
+    // ---- lidar + is_collision2 (ffmp.py:108-117) ----
+    bool c_lidar = false;
+    for (int l = lane; l < L; l += 64) {
+      const double r = lidar_beam(cfg, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
+                                  s_ox, s_oy, s_or, K);
+      const float rf = (float)r;
+      ob.lidar[e * L + l] = rf;
+      c_lidar |= beam_collides(rf, cfg.robot_r);
+    }
+    c_foot = __any(c_foot);
+    c_lidar = __any(c_lidar) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
+    col = c_foot || c_lidar;
+    // ---- is_goal / reward / is_done (ffmp.py:120-164), truncation (train.py:607) ----
+    goal = dist < cfg.goal_thr;
+    reward = reward_calc(dist, d0, col, goal);
+    trunc = (cfg.max_steps > 0) && (t >= cfg.max_steps);
+    done = col || goal || trunc;
+    reset_now = done && cfg.autoreset;
+    if (!reset_now) {
+      // small obs of the post-step state
+      if (lane == 0) {
+        ob.state_g[e * 2 + 0] = (float)dist;
+        ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
+      }
+    }
+  }
+
+  if (reset_now) {
+    // ---- episode reset (the external /episode_manager; train.py:559-566) ----
+    episode = (MODE == kEnvMode_Reset && initial) ? 0 : episode + 1;
+    const Episode ep = sample_episode(cfg, genv, episode);
+    x1 = ep.x; y1 = ep.y; yaw1 = ep.yaw; gx = ep.gx; gy = ep.gy;
+    __syncthreads();  // all lanes done reading the terminal-state LDS arrays
+    if (has_obst) my = sample_obstacle(cfg, genv, episode, lane, ep);
+    c1 = cos(yaw1); s1 = sin(yaw1);
+    if (has_obst) {
+      s_ox[lane] = my.x; s_oy[lane] = my.y; s_or[lane] = my.r;
+      const float4 eo = ego_obst(my, x1, y1, c1, s1);
+      s_ecur[lane] = eo;
+      s_eprev[lane] = eo;  // temporal stack duplicated on the first step (train.py:475-478)
+    }
+    __syncthreads();
+    hcur = make_hdr(x1, y1, c1, s1);
+    hprev = hcur;
+    t = 0;
+    vlin = 0.0; vang = 0.0;  // robot_velocity_calculator with is_first (train.py:183-184)
+    t_obs = 0.0f;            // odom dt on the first step (train.py:532-533,540)
+    const double dx = gx - x1, dy = gy - y1;
+    const double dist = sqrt(dx * dx + dy * dy);
+    d0 = dist;  // pre_relative_goal_dist on is_first (ffmp.py:139-141)
+    if (lane == 0) {
+      ob.state_g[e * 2 + 0] = (float)dist;
+      ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
+    }
+    for (int l = lane; l < L; l += 64) {
+      const double r = lidar_beam(cfg, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
+                                  s_ox, s_oy, s_or, K);
+      ob.lidar[e * L + l] = (float)r;
+    }
+  }
+
+  // ---- field-gradient lookup at the robot cell (central differences) ----
+  {
+    const float2 ge = to_ego(gx, gy, x1, y1, c1, s1);
+    float U = 0.0f;
+    if (lane < 4) {
+      const int di = (lane == 0) ? 1 : (lane == 1) ? -1 : 0;
+      const int dj = (lane == 2) ? 1 : (lane == 3) ? -1 : 0;
+      U = potential_cell(cfg, s_ecur, K, ge.x, ge.y, ic + di, ic + dj);
+    }
+    const float Uxp = __shfl(U, 0), Uxm = __shfl(U, 1), Uyp = __shfl(U, 2), Uym = __shfl(U, 3);
+    float* rec = st.record + e * rec_stride(K);
+    if (lane == 0) {
+      ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
+      ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
+      rec[8] = ge.x;
+      rec[9] = ge.y;
+      rec[10] = 0.0f;
+      rec[11] = 0.0f;
+    }
+    if (lane < 4) {
+      rec[lane] = lane == 0 ? hcur.px : lane == 1 ? hcur.py : lane == 2 ? hcur.c : hcur.s;
+      rec[4 + lane] = lane == 0 ? hprev.px : lane == 1 ? hprev.py : lane == 2 ? hprev.c : hprev.s;
+      rec[12 + lane] = 0.0f;
+    }
+    if (has_obst) {
+      float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
+      ro[lane] = s_ecur[lane];
+      ro[K + lane] = s_eprev[lane];
+    }
+  }
+
+  // ---- write back state / obs / outputs ----
+  if (has_obst) {
+    double* p = st.obst + (e * K + lane) * 4;
+    p[0] = my.x; p[1] = my.y; p[2] = my.vx; p[3] = my.vy;
+    st.obst_r[e * K + lane] = my.r;
+  }
+  if (lane == 0) {
+    st.pose[e * 3 + 0] = x1; st.pose[e * 3 + 1] = y1; st.pose[e * 3 + 2] = yaw1;
+    st.goal[e * 2 + 0] = gx; st.goal[e * 2 + 1] = gy;
+    st.d0[e] = d0;
+    st.t[e] = t;
+    st.episode[e] = episode;
+    ob.state_v[e * 2 + 0] = (float)vlin;
+    ob.state_v[e * 2 + 1] = (float)vang;
+    ob.state_t[e] = t_obs;
+    if (MODE == kEnvMode_Step) {
+      out.reward[e] = (float)reward;
+      out.done[e] = done;
+      out.is_goal[e] = goal;
+      out.collide[e] = col;
+      out.truncated[e] = trunc;
+    }
+  }
+}
+
+// ============================================================================
+// raster_kernel: the HBM-bound hot path.
+//   block = 256 threads (4 waves); a pass covers 1024 consecutive cells of one
+//   env plane (each wave a contiguous 256-cell chunk, each lane 4 cells = one
+//   16-B store per plane).  Obstacles of both frames sit in LDS; per chunk a
+//   wave-uniform bitmask keeps only those whose disc (occupancy) or repulsive
+//   reach (potential) can touch the chunk's ego bounding box, and the world
+//   wall test is skipped when the chunk's four corners are safely inside.
+// ============================================================================
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+FFMP_DEV void store_nt(float* p, float a, float b, float c, float d) {
+  f32x4 v = {a, b, c, d};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
+
+struct ChunkCull {
+  uint64_t mask;
+  bool walls;  // per-cell wall test needed
+};
+
+FFMP_DEV float box_dist2(float px, float py, float x0, float x1, float y0, float y1) {
+  const float dx = fmaxf(fmaxf(x0 - px, px - x1), 0.0f);
+  const float dy = fmaxf(fmaxf(y0 - py, py - y1), 0.0f);
+  return dx * dx + dy * dy;
+}
+
+FFMP_DEV bool corner_inside(const ffmp_cfg_t& cfg, const FrameHdr& h, float ex, float ey) {
+  const float wx = h.px + (h.c * ex - h.s * ey);
+  const float wy = h.py + (h.s * ex + h.c * ey);
+  const float W = cfg.world_half_f - cfg.cull_margin_f;
+  return (fabsf(wx) <= W) && (fabsf(wy) <= W);
+}
+
+FFMP_DEV ChunkCull cull_chunk(const ffmp_cfg_t& cfg, const FrameHdr& h, const float4* obs, int K,
+                              float reach_extra, float x0, float x1, float y0, float y1) {
+  ChunkCull cc;
+  uint64_t m = 0;
+  for (int k = 0; k < K; ++k) {
+    const float4 o = obs[k];
+    const float reach = o.w + reach_extra;
+    if (box_dist2(o.x, o.y, x0, x1, y0, y1) <= reach * reach) m |= (1ull << k);
+  }
+  cc.mask = m;
+  cc.walls = !(corner_inside(cfg, h, x0, y0) && corner_inside(cfg, h, x0, y1) &&
+               corner_inside(cfg, h, x1, y0) && corner_inside(cfg, h, x1, y1));
+  return cc;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
+                                                     int32_t cells_per_block,
+                                                     const float* __restrict__ record,
+                                                     const uint8_t* __restrict__ mask,
+                                                     float* __restrict__ state_m,
+                                                     float* __restrict__ pot) {
+  __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
+  __shared__ float s_hdr[FFMP_REC_HDR];
+
+  const int64_t e = blockIdx.x / bpe;
+  const int tile = (int)(blockIdx.x - e * bpe);
+  if (e >= n) return;
+  if (mask && !mask[e]) return;
+
+  const int K = cfg.n_obst;
+  const int G = cfg.grid;
+  const int G2 = G * G;
+  const int tid = threadIdx.x;
+  const float* rec = record + e * rec_stride(K);
+  if (tid < FFMP_REC_HDR) s_hdr[tid] = rec[tid];
+  if (tid < K) {
+    const float4* ro = reinterpret_cast<const float4*>(rec + FFMP_REC_HDR);
+    s_cur[tid] = ro[tid];
+    s_prev[tid] = ro[K + tid];
+  }
+  __syncthreads();
+
+  const FrameHdr hc{s_hdr[0], s_hdr[1], s_hdr[2], s_hdr[3]};
+  const FrameHdr hp{s_hdr[4], s_hdr[5], s_hdr[6], s_hdr[7]};
+  const float gx = s_hdr[8], gy = s_hdr[9];
+  const float res = cfg.res_f, half = cfg.half_f;
+  const float pot_reach = cfg.rho0_f + cfg.cull_margin_f;
+
+  float* m0 = state_m + (int64_t)e * 2 * G2;
+  float* m1 = m0 + G2;
+  float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int qbeg = tile * cells_per_block;
+  const int qend = min(qbeg + cells_per_block, G2);
+
+  for (int q0 = qbeg + wave * 256; q0 < qend; q0 += 1024) {
+    // ---- wave chunk [q0, qlast] -> ego bounding box ----
+    const int qlast = min(q0 + 255, G2 - 1);
+    const int i0 = q0 / G, i1 = qlast / G;
+    int j0 = 0, j1 = G - 1;
+    if (i0 == i1) { j0 = q0 - i0 * G; j1 = qlast - i0 * G; }
+    const float bx0 = (float)i0 * res - half, bx1 = (float)i1 * res - half;
+    const float by0 = (float)j0 * res - half, by1 = (float)j1 * res - half;
+    const ChunkCull cc = cull_chunk(cfg, hc, s_cur, K, pot_reach, bx0, bx1, by0, by1);
+    const ChunkCull cp = cull_chunk(cfg, hp, s_prev, K, cfg.cull_margin_f, bx0, bx1, by0, by1);
+    const uint64_t mc = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc.mask >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cc.mask);
+    const uint64_t mp = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cp.mask >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cp.mask);
+
+    const int q = q0 + lane * 4;
+    if (q >= qend) continue;
+    const int i = q / G;
+    const int j = q - i * G;
+    const float ex = (float)i * res - half;
+    float ey[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ey[u] = (float)(j + u) * res - half;
+
+    float occp[4], occc[4], U[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      occp[u] = (cp.walls && outside_world(cfg, hp, ex, ey[u])) ? 1.0f : 0.0f;
+      occc[u] = (cc.walls && outside_world(cfg, hc, ex, ey[u])) ? 1.0f : 0.0f;
+      U[u] = attractive(cfg, ex, ey[u], gx, gy);
+    }
+    for (uint64_t m = mp; m; m &= m - 1) {
+      const float4 o = s_prev[__builtin_ctzll(m)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) if (in_disc(ex, ey[u], o)) occp[u] = 1.0f;
+    }
+    for (uint64_t m = mc; m; m &= m - 1) {
+      const float4 o = s_cur[__builtin_ctzll(m)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (in_disc(ex, ey[u], o)) occc[u] = 1.0f;
+        U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
+      }
+    }
+    store_nt(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
+    store_nt(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
+    if (pp) store_nt(pp + q, U[0], U[1], U[2], U[3]);
+  }
+}
+
+// ============================================================================
+// Legacy FFMP methods as batched kernels (one thread per env).
+// ============================================================================
+__global__ void reward_done_kernel(ffmp_cfg_t cfg, int64_t n, const double* __restrict__ scan,
+                                   int32_t scan_len, const float* __restrict__ local_map,
+                                   int64_t map_stride, const uint8_t* __restrict__ collide_in,
+                                   const uint8_t* __restrict__ goal_in,
+                                   const double* __restrict__ rel_goal,
+                                   const uint8_t* __restrict__ is_first, double* d0, double* reward,
+                                   uint8_t* done, uint8_t* is_goal, uint8_t* collide) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  bool col = collide_in ? (collide_in[e] != 0) : false;
+  if (scan) {
+    for (int l = 0; l < scan_len; ++l) {
+      const double r = scan[e * scan_len + l];
+      if (r != 0.0 && r < cfg.robot_r) { col = true; break; }
+    }
+  }
+  if (local_map) {
+    const float* m = local_map + e * map_stride;
+    const int c = cfg.grid / 2;
+    for (int f = 0; f < cfg.n_foot; ++f)
+      if (m[(int64_t)(c + cfg.foot_di[f]) * cfg.grid + (c + cfg.foot_dj[f])] > 0.0f) { col = true; break; }
+  }
+  const double dist = rel_goal[e * 2];
+  const bool goal = goal_in ? (goal_in[e] != 0) : (dist < cfg.goal_thr);
+  if (is_first[e]) d0[e] = dist;
+  reward[e] = reward_calc(dist, d0[e], col, goal);
+  done[e] = col || goal;
+  is_goal[e] = goal;
+  collide[e] = col;
+}
+
+__global__ void footprint_kernel(ffmp_cfg_t cfg, int64_t n, const float* __restrict__ local_map,
+                                 int64_t map_stride, uint8_t* collide) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* m = local_map + e * map_stride;
+  const int c = cfg.grid / 2;
+  bool col = false;
+  for (int f = 0; f < cfg.n_foot; ++f)
+    col |= m[(int64_t)(c + cfg.foot_di[f]) * cfg.grid + (c + cfg.foot_dj[f])] > 0.0f;
+  collide[e] = col;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void scan_kernel(int64_t n, int32_t L, const T* __restrict__ ranges,
+                                                   double thr, uint8_t* collide, T* min_r) {
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= n) return;
+  bool col = false;
+  T mn = (T)__builtin_inf();
+  for (int l = lane; l < L; l += 64) {
+    const T r = ranges[e * L + l];
+    if (r != (T)0) {
+      col |= (double)r < thr;
+      mn = r < mn ? r : mn;  // NaN never replaces
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const T o = __shfl_xor(mn, off);
+    mn = o < mn ? o : mn;
+  }
+  col = __any(col);
+  if (lane == 0) {
+    collide[e] = col;
+    if (min_r) min_r[e] = mn;
+  }
+}
+
+template <typename T>
+int scan_impl(int64_t n, int32_t L, const T* ranges, double thr, uint8_t* collide, T* min_r,
+                     void* stream) {
+  if (n < 0 || L < 0) return fail(FFMP_E_ARG, "negative n or L");
+  if ((L > 0 && !ranges) || !collide) return fail(FFMP_E_ARG, "ranges/collide is NULL");
+  if (n == 0) return FFMP_OK;
+  hipLaunchKernelGGL(scan_kernel<T>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n, L,
+                     ranges, thr, collide, min_r);
+  return check_launch("ffmp_scan_collision");
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int ffmp_abi_version(void) { return FFMP_ABI_VERSION; }
+const char* ffmp_last_error(void) { return g_err; }
+
+int64_t ffmp_layout(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(ffmp_cfg_t);
+    case 1: return (int64_t)sizeof(ffmp_state_t);
+    case 2: return (int64_t)sizeof(ffmp_obs_t);
+    case 3: return (int64_t)sizeof(ffmp_out_t);
+    case 4: return (int64_t)offsetof(ffmp_cfg_t, res);
+    case 5: return (int64_t)offsetof(ffmp_cfg_t, res_f);
+    case 6: return (int64_t)offsetof(ffmp_cfg_t, seed);
+    case 7: return (int64_t)offsetof(ffmp_cfg_t, beam_cs);
+    default: return -1;
+  }
+}
+
+int ffmp_footprint(int32_t grid, double res, double robot_r, int32_t* di, int32_t* dj, int32_t cap) {
+  if (grid <= 0 || !(res > 0.0)) return fail(FFMP_E_ARG, "bad grid/res");
+  // ffmp.py:87-94 with map_range = grid * res: cells whose corner-index
+  // position lies within robot_r of the map centre.  Only a window around the
+  // centre can qualify; scanning it in (i, j) order reproduces the list order.
+  const double map_range = (double)grid * res;
+  const int w = (int)ceil(robot_r / res) + 2;
+  const int c = grid / 2;
+  int cnt = 0;
+  for (int i = c - w; i <= c + w; ++i) {
+    if (i < 0 || i >= grid) continue;
+    for (int j = c - w; j <= c + w; ++j) {
+      if (j < 0 || j >= grid) continue;
+      const double xp = pow(i * res - 0.5 * map_range, 2.0);
+      const double yp = pow(j * res - 0.5 * map_range, 2.0);
+      if (sqrt(xp + yp) <= robot_r) {
+        if (cnt < cap && di && dj) { di[cnt] = i - c; dj[cnt] = j - c; }
+        ++cnt;
+      }
+    }
+  }
+  return cnt;
+}
+
+static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
+                      const int64_t* action, const uint8_t* mask, int32_t initial,
+                      ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0 || env_offset < 0) return fail(FFMP_E_ARG, "negative n or env_offset");
+  if (!state || !obs) return fail(FFMP_E_ARG, "state/obs is NULL");
+  if (!state->pose || !state->goal || !state->d0 || !state->t || !state->episode || !state->record || !state->err)
+    return fail(FFMP_E_ARG, "a state pointer is NULL");
+  if (cfg->n_obst > 0 && (!state->obst || !state->obst_r)) return fail(FFMP_E_ARG, "obstacle state NULL");
+  if (!obs->state_g || !obs->state_v || !obs->state_t || !obs->grad)
+    return fail(FFMP_E_ARG, "an obs pointer is NULL");
+  if (cfg->n_beams > 0 && !obs->lidar) return fail(FFMP_E_ARG, "obs.lidar NULL with n_beams > 0");
+  if (mode == kEnvMode_Step) {
+    if (!action) return fail(FFMP_E_ARG, "action is NULL");
+    if (!out || !out->reward || !out->done || !out->is_goal || !out->collide || !out->truncated)
+      return fail(FFMP_E_ARG, "an out pointer is NULL");
+  }
+  if (n == 0) return FFMP_OK;
+  if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
+  ffmp_out_t o = out ? *out : ffmp_out_t{};
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == kEnvMode_Step)
+    hipLaunchKernelGGL(env_kernel<kEnvMode_Step>, dim3((unsigned)n), dim3(64), 0, s, *cfg, n, env_offset,
+                       action, mask, initial, *state, *obs, o);
+  else
+    hipLaunchKernelGGL(env_kernel<kEnvMode_Reset>, dim3((unsigned)n), dim3(64), 0, s, *cfg, n, env_offset,
+                       action, mask, initial, *state, *obs, o);
+  return check_launch(mode == kEnvMode_Step ? "ffmp_step_state" : "ffmp_reset");
+}
+
+int ffmp_reset(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const uint8_t* mask,
+               int32_t initial, ffmp_state_t* state, ffmp_obs_t* obs, void* stream) {
+  return launch_env(kEnvMode_Reset, cfg, n, env_offset, nullptr, mask, initial, state, obs, nullptr, stream);
+}
+
+int ffmp_step_state(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,
+                    ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, void* stream) {
+  return launch_env(kEnvMode_Step, cfg, n, env_offset, action, nullptr, 0, state, obs, out, stream);
+}
+
+int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uint8_t* mask,
+                ffmp_obs_t* obs, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (!record || !obs || !obs->state_m) return fail(FFMP_E_ARG, "record/obs/state_m is NULL");
+  if (n == 0) return FFMP_OK;
+  const int G2 = cfg->grid * cfg->grid;
+  const int cpb = G2 < 8192 ? ((G2 + 1023) / 1024) * 1024 : 8192;
+  const int bpe = (G2 + cpb - 1) / cpb;
+  const int64_t blocks = n * bpe;
+  if (blocks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many raster blocks: %lld", (long long)blocks);
+  hipLaunchKernelGGL(raster_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
+                     bpe, cpb, record, mask, obs->state_m, obs->potential);
+  return check_launch("ffmp_raster");
+}
+
+int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,
+              ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, void* stream) {
+  int rc = ffmp_step_state(cfg, n, env_offset, action, state, obs, out, stream);
+  if (rc) return rc;
+  return ffmp_raster(cfg, n, state->record, nullptr, obs, stream);
+}
+
+int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n, const double* scan, int32_t scan_len,
+                     const float* local_map, int64_t map_stride, const uint8_t* collide_in,
+                     const uint8_t* goal_in, const double* rel_goal, const uint8_t* is_first,
+                     double* d0, double* reward, uint8_t* done, uint8_t* is_goal, uint8_t* collide,
+                     void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0 || scan_len < 0) return fail(FFMP_E_ARG, "negative n or scan_len");
+  if (!rel_goal || !is_first || !d0 || !reward || !done || !is_goal || !collide)
+    return fail(FFMP_E_ARG, "a required pointer is NULL");
+  if (n == 0) return FFMP_OK;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(reward_done_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n, scan,
+                     scan_len, local_map, map_stride, collide_in, goal_in, rel_goal, is_first, d0, reward,
+                     done, is_goal, collide);
+  return check_launch("ffmp_reward_done");
+}
+
+int ffmp_footprint_collision(const ffmp_cfg_t* cfg, int64_t n, const float* local_map, int64_t map_stride,
+                             uint8_t* collide, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (!local_map || !collide) return fail(FFMP_E_ARG, "local_map/collide is NULL");
+  if (n == 0) return FFMP_OK;
+  hipLaunchKernelGGL(footprint_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     *cfg, n, local_map, map_stride, collide);
+  return check_launch("ffmp_footprint_collision");
+}
+
+int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr, uint8_t* collide, float* min_r,
+                        void* stream) {
+  return scan_impl<float>(n, L, ranges, thr, collide, min_r, stream);
+}
+
+int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr, uint8_t* collide,
+                            double* min_r, void* stream) {
+  return scan_impl<double>(n, L, ranges, thr, collide, min_r, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+/*
+ * ffmp.h — C ABI of libffmp, the MI355X (gfx950) batched flow-field
+ * motion-planning environment (the `gym_ffmp` step/reset hot path).
+ *
+ * Every buffer is caller-owned, contiguous, env-major DEVICE memory (in
+ * practice torch tensors' data_ptr()).  Nothing here allocates, prints or
+ * throws.  Each call enqueues work on `stream` (a hipStream_t passed as void*;
+ * NULL = the legacy default stream) and returns 0, or a negative FFMP_E_* code
+ * with a message readable from ffmp_last_error() (thread-local).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repo YoshitakaNagai/flow_field_based_motion_planner):
+ *   ffmp_reset          -> the external /episode_manager + is_first branch of
+ *                          src/train.py:532-566 (start/goal, temporal stack
+ *                          duplication, velocity := 0, d0 := dist) and the
+ *                          commented-out FFMP.reset src/gym_ffmp/envs/ffmp.py:77-83
+ *   ffmp_step           -> one iteration of src/train.py:523-693 with Gazebo
+ *                          (/cmd_vel integration), /bev_* rasterisers and
+ *                          rewarder2 (src/gym_ffmp/envs/ffmp.py:179-188) in-GPU
+ *   ffmp_raster         -> external /bev_flow_estimator + /temporal_bev_publisher
+ *                          (src/train.py:116-121, make_temporal_maps :474-486)
+ *   ffmp_reward_done    -> FFMP.rewarder / rewarder2 / reward_calculator /
+ *                          is_goal / is_done (src/gym_ffmp/envs/ffmp.py:120-188)
+ *   ffmp_footprint_collision -> FFMP.is_collision (ffmp.py:85-105)
+ *   ffmp_scan_collision[_f64] -> FFMP.is_collision2 (ffmp.py:108-117)
+ *   ffmp_footprint      -> the robot_grids mask built inside is_collision
+ *                          (ffmp.py:87-94), host-side, float64
+ */
+#ifndef FFMP_H
+#define FFMP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFMP_ABI_VERSION 1
+#define FFMP_MAX_OBST 64     /* K  */
+#define FFMP_MAX_FOOT 128    /* footprint cells */
+#define FFMP_MAX_BEAMS 1024  /* L  */
+#define FFMP_N_ACTIONS 28
+#define FFMP_REC_HDR 16      /* floats of per-env raster-record header */
+
+/* error codes */
+#define FFMP_OK 0
+#define FFMP_E_ARG (-1)
+#define FFMP_E_HIP (-2)
+#define FFMP_E_CFG (-3)
+
+/* collide_mode bits */
+#define FFMP_COLLIDE_FOOTPRINT 1
+#define FFMP_COLLIDE_LIDAR 2
+
+/* Configuration, passed by pointer and copied by value into each launch.
+ * float64 fields drive the per-env scalar maths (as the reference's Python
+ * floats do); the *_f fields are the float32 constants of the per-cell raster
+ * and MUST equal (float)(the double expression) documented beside them — the
+ * Python host (flow_field_based_motion_planner_amd/config.py) fills both. */
+typedef struct ffmp_cfg {
+  int32_t grid;          /* G: local map is G x G cells, G % 4 == 0, 8 <= G <= 4096 */
+  int32_t n_obst;        /* K: obstacles per env, 0..FFMP_MAX_OBST */
+  int32_t n_beams;       /* L: lidar beams, 0..FFMP_MAX_BEAMS (0 = no lidar) */
+  int32_t max_steps;     /* truncation: done when t == max_steps (train.py:60,607) */
+  int32_t moving;        /* 1: obstacles move and reflect off the world walls */
+  int32_t autoreset;     /* 1: ffmp_step resets done envs in place */
+  int32_t collide_mode;  /* FFMP_COLLIDE_* bits */
+  int32_t n_foot;        /* number of footprint offsets below */
+  int32_t foot_di[FFMP_MAX_FOOT]; /* footprint cell offsets from (G/2, G/2) */
+  int32_t foot_dj[FFMP_MAX_FOOT];
+  double res;            /* m per cell (ffmp.py:18, 0.05) */
+  double dt;             /* s per step */
+  double robot_r;        /* lidar collision threshold (ffmp.py:17, 0.13) */
+  double goal_thr;       /* goal threshold (ffmp.py:19, 0.5) */
+  double world_half;     /* world is [-world_half, world_half]^2 (m) */
+  double lidar_max;      /* lidar max range (m); farther -> +inf */
+  double goal_min, goal_max;   /* reset: goal distance range (m) */
+  double obst_rmin, obst_rmax; /* reset: obstacle radius range (m) */
+  double obst_vmax;            /* reset: obstacle speed range [0, vmax] (moving) */
+  double start_clear, goal_clear; /* reset: clearance of obstacle surface from start / goal */
+  /* float32 raster constants */
+  float res_f;           /* (float)res */
+  float half_f;          /* (float)(0.5 * (G * res)) : ego coordinate of cell 0 is -half_f */
+  float world_half_f;    /* (float)world_half */
+  float half_ka_f;       /* (float)(0.5 * k_att) */
+  float half_kr_f;       /* (float)(0.5 * k_rep) */
+  float rho0_f;          /* (float)rho0 : repulsive cut-off (m) */
+  float inv_rho0_f;      /* (float)(1.0 / rho0) */
+  float rho_min_f;       /* (float)rho_min : distance clamp (m) */
+  float inv_2res_f;      /* (float)(1.0 / (2.0 * res)) : central-difference scale */
+  float cull_margin_f;   /* extra culling margin (m), conservative */
+  uint64_t seed;         /* Philox4x32-10 key */
+  const double* beam_cs; /* DEVICE (L,2) float64 {cos, sin} of beam angle -pi + l*2pi/L */
+} ffmp_cfg_t;
+
+/* Per-env simulator state (device pointers, N envs). */
+typedef struct ffmp_state {
+  double* pose;     /* (N,3) x, y, yaw                               */
+  double* goal;     /* (N,2) world goal                              */
+  double* d0;       /* (N)   pre_relative_goal_dist (ffmp.py:139)    */
+  double* obst;     /* (N,K,4) x, y, vx, vy                          */
+  double* obst_r;   /* (N,K) radius                                  */
+  int32_t* t;       /* (N)   steps since episode start               */
+  int32_t* episode; /* (N)   episode counter (RNG key part)          */
+  float* record;    /* (N, FFMP_REC_HDR + 8K) raster record */
+  uint32_t* err;    /* (1)   sticky error bits (bit0: bad action id) */
+} ffmp_state_t;
+
+/* Observation tensors (device pointers).  Layout = reference train.py:44,543-557
+ * with a leading N: state_m (N,2,G,G) [older, newest] values 0/255 as float. */
+typedef struct ffmp_obs {
+  float* state_m;   /* (N,2,G,G) */
+  float* state_g;   /* (N,2) relative goal [dist, orient]          */
+  float* state_v;   /* (N,2) per-step [|dxy|, wrap(dyaw)]          */
+  float* state_t;   /* (N,1) dt (0 on the first step)              */
+  float* potential; /* (N,G,G) attractive+repulsive potential, or NULL */
+  float* grad;      /* (N,2) central-difference gradient at robot cell */
+  float* lidar;     /* (N,L) ranges (+inf = no return, -inf = inside), NULL if L == 0 */
+} ffmp_obs_t;
+
+/* Per-step outputs (device pointers, N each). Flags are 0/1 bytes. */
+typedef struct ffmp_out {
+  float* reward;
+  uint8_t* done;
+  uint8_t* is_goal;
+  uint8_t* collide;
+  uint8_t* truncated;
+} ffmp_out_t;
+
+int ffmp_abi_version(void);
+const char* ffmp_last_error(void);
+
+/* Layout check for FFI bindings: which = 0 sizeof(ffmp_cfg_t), 1 sizeof(ffmp_state_t),
+ * 2 sizeof(ffmp_obs_t), 3 sizeof(ffmp_out_t), 4 offsetof(ffmp_cfg_t, res),
+ * 5 offsetof(ffmp_cfg_t, res_f), 6 offsetof(ffmp_cfg_t, seed),
+ * 7 offsetof(ffmp_cfg_t, beam_cs); -1 otherwise. */
+int64_t ffmp_layout(int32_t which);
+
+/* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G
+ * (map_range = G*res).  Writes up to `cap` offsets (cell - G/2); returns the
+ * count, or a negative code. */
+int ffmp_footprint(int32_t grid, double res, double robot_r,
+                   int32_t* di, int32_t* dj, int32_t cap);
+
+/* Reset envs [0,n) (global index env_offset + e) where mask[e] != 0 (mask NULL
+ * = all).  initial != 0: episode := 0, else episode += 1.  Writes state, the
+ * small obs (g, v=0, t=0, grad, lidar) and the raster record; call ffmp_raster
+ * (same mask) afterwards for state_m / potential. */
+int ffmp_reset(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
+               const uint8_t* mask, int32_t initial,
+               ffmp_state_t* state, ffmp_obs_t* obs, void* stream);
+
+/* One env step for envs [0,n): action[e] in 0..27 (int64, train.py:343-345).
+ * Integrates, moves obstacles, lidar, collision/goal/reward/done, truncation,
+ * auto-reset (cfg.autoreset), small obs and raster record.  Does NOT raster. */
+int ffmp_step_state(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
+                    const int64_t* action, ffmp_state_t* state, ffmp_obs_t* obs,
+                    ffmp_out_t* out, void* stream);
+
+/* Raster state_m[:,0] (previous frame), state_m[:,1] (current frame) and the
+ * potential plane from the raster record (mask NULL = all envs). */
+int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
+                const uint8_t* mask, ffmp_obs_t* obs, void* stream);
+
+/* ffmp_step_state + ffmp_raster. */
+int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
+              const int64_t* action, ffmp_state_t* state, ffmp_obs_t* obs,
+              ffmp_out_t* out, void* stream);
+
+/* Standalone reward/done (FFMP.rewarder / rewarder2 semantics), n envs:
+ *   scan:   (n, scan_len) float64 ranges (0 = skipped, as `if scan_data[i]`), or NULL
+ *   local_map: float32 planes, env e at local_map + e*map_stride (G x G), or NULL
+ *   collide_in: optional precomputed collision bytes (used when scan and map are NULL)
+ *   goal_in: optional precomputed goal bytes (NULL: dist < goal_thr)
+ *   rel_goal (n,2) float64, is_first (n) bytes, d0 (n) float64 in/out.
+ * Outputs reward (n) float64, done / is_goal / collide (n) bytes. */
+int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n,
+                     const double* scan, int32_t scan_len,
+                     const float* local_map, int64_t map_stride,
+                     const uint8_t* collide_in, const uint8_t* goal_in,
+                     const double* rel_goal, const uint8_t* is_first, double* d0,
+                     double* reward, uint8_t* done, uint8_t* is_goal, uint8_t* collide,
+                     void* stream);
+
+/* FFMP.is_collision: any local_map[(G/2+di), (G/2+dj)] > 0 over the footprint. */
+int ffmp_footprint_collision(const ffmp_cfg_t* cfg, int64_t n, const float* local_map,
+                             int64_t map_stride, uint8_t* collide, void* stream);
+
+/* FFMP.is_collision2 over (n, L) ranges: collide = any(r != 0 && r < thr);
+ * min_r = min over those beams (+inf if none), may be NULL. */
+int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr,
+                        uint8_t* collide, float* min_r, void* stream);
+int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr,
+                            uint8_t* collide, double* min_r, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FFMP_H */

@@ -1,0 +1,37 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libffmp on cuda:0)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLDEN, "ref_pinned.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_maps():
+    with np.load(os.path.join(GOLDEN, "ref_maps.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def lib():
+    """The built libffmp (host entry points work without a GPU)."""
+    import __graft_entry__
+    __graft_entry__.build()
+    from flow_field_based_motion_planner_amd import _abi
+    return _abi.load()

@@ -1,0 +1,320 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors that pin the oracle to the reference.
+
+RUNS ONLY IN THE BUILD CONTAINER (it needs /root/reference, which never travels
+to the GPU box).  It imports the reference's own code at run time and records
+INPUTS and OUTPUTS only; no reference source is copied into this repository.
+
+What is driven (reference file:line):
+  * gym_ffmp.envs.ffmp.FFMP  (src/gym_ffmp/envs/ffmp.py:22-188)
+      is_collision (:85-105), is_collision2 (:108-117), is_goal (:120-127),
+      reward_calculator (:130-157, incl. the module-global d0 and the
+      NameError before the first is_first), is_done (:160-164),
+      rewarder (:167-176), rewarder2 (:179-188)
+  * RobotAction.cmd (src/gym_ffmp/envs/robot/config.py:25-58)
+  * train.py helpers, compiled from the reference file's AST without importing
+    rospy: ROSNode.pi_to_pi (:167-172), relative_goal_calculator (:174-180),
+    robot_velocity_calculator (:182-188), Environment.make_temporal_maps
+    (:474-486).
+
+`gym` is not installed here (nor on the GPU box), so a minimal offline stand-in
+(this file's own code: Env, spaces.Box/Dict, envs.registration.register) is
+written to a temp dir and put on sys.path before the reference is imported.
+
+Usage:  python tests/golden/make_golden.py      (writes ref_pinned.json, ref_maps.npz)
+"""
+import ast
+import contextlib
+import copy
+import io
+import json
+import math
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+REF_SRC = "/root/reference/src"
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+
+_GYM_STANDIN = {
+    "gym/__init__.py": (
+        "from . import spaces, error, utils, envs\n"
+        "class Env(object):\n"
+        "    pass\n"
+        "def make(env_id):\n"
+        "    return envs.registration._REG[env_id]()\n"
+    ),
+    "gym/error.py": "",
+    "gym/utils/__init__.py": "from . import seeding\n",
+    "gym/utils/seeding.py": "",
+    "gym/envs/__init__.py": "from . import registration\n",
+    "gym/envs/registration.py": (
+        "_REG = {}\n"
+        "def register(id, entry_point, **kw):\n"
+        "    mod, name = entry_point.split(':')\n"
+        "    def _mk():\n"
+        "        import importlib\n"
+        "        return getattr(importlib.import_module(mod), name)()\n"
+        "    _REG[id] = _mk\n"
+    ),
+    "gym/spaces.py": (
+        "import numpy as np\n"
+        "class Box(object):\n"
+        "    def __init__(self, low, high, dtype=np.float32, shape=None):\n"
+        "        self.low = np.asarray(low); self.high = np.asarray(high); self.dtype = dtype\n"
+        "        self.shape = self.low.shape\n"
+        "class Dict(object):\n"
+        "    def __init__(self, d):\n"
+        "        self.spaces = dict(d)\n"
+    ),
+}
+
+
+def _install_gym_standin():
+    root = tempfile.mkdtemp(prefix="gym_standin_")
+    for rel, txt in _GYM_STANDIN.items():
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            f.write(txt)
+    sys.path.insert(0, root)
+    sys.path.insert(0, REF_SRC)
+
+
+def _train_helpers():
+    """Compile four helper methods out of the reference train.py AST."""
+    import torch
+    with open(os.path.join(REF_SRC, "train.py")) as f:
+        tree = ast.parse(f.read())
+    want = {("ROSNode", "pi_to_pi"), ("ROSNode", "relative_goal_calculator"),
+            ("ROSNode", "robot_velocity_calculator"), ("Environment", "make_temporal_maps")}
+    fns = []
+    for node in tree.body:
+        if isinstance(node, ast.ClassDef):
+            for sub in node.body:
+                if isinstance(sub, ast.FunctionDef) and (node.name, sub.name) in want:
+                    fns.append(sub)
+    mod = ast.Module(body=fns, type_ignores=[])
+    g = {"math": math, "np": np, "copy": copy, "torch": torch, "INPUT_CHANNELS": 2}
+    exec(compile(mod, "<reference train.py helpers>", "exec"), g)
+    return g
+
+
+class _Pose(object):
+    def __init__(self, x, y, yaw):
+        self.x, self.y, self.yaw = x, y, yaw
+
+
+def main():
+    _install_gym_standin()
+    import gym_ffmp  # noqa: F401  (registers FFMP-v0 with the stand-in)
+    from gym_ffmp.envs import ffmp as ffmp_mod
+    from gym_ffmp.envs.ffmp import FFMP
+    from gym_ffmp.envs.robot.config import RobotAction
+
+    rng = np.random.default_rng(20240601)
+    out = {"generator": "tests/golden/make_golden.py", "reference": "YoshitakaNagai/flow_field_based_motion_planner"}
+    maps = {}
+
+    # ---- NameError before the first is_first (must run before any reward call) ----
+    env = FFMP()
+    try:
+        env.reward_calculator(np.array([1.0, 0.0]), False, False, False)
+        out["reward_nameerror"] = False
+    except NameError:
+        out["reward_nameerror"] = True
+
+    # ---- module constants / spaces ----
+    out["constants"] = {
+        "MAP_RANGE": ffmp_mod.MAP_RANGE, "MAP_GRID_NUM": ffmp_mod.MAP_GRID_NUM,
+        "ROBOT_RSIZE": ffmp_mod.ROBOT_RSIZE, "MAP_RESOLUTION": ffmp_mod.MAP_RESOLUTION,
+        "GOAL_THRESHOLHD": ffmp_mod.GOAL_THRESHOLHD,
+        "action_low": env.action_low.tolist(), "action_high": env.action_high.tolist(),
+        "goal_high": env.goal_high.tolist(),
+    }
+    act = RobotAction()
+    out["action_table"] = [[c.linear_v, c.angular_v] for c in act.cmd]
+
+    # ---- footprint cells for several G (generalised map_range = G * res) ----
+    out["footprint"] = {}
+    for G in (64, 100, 128, 256, 512):
+        e = FFMP()
+        if G != 100:
+            e.map_grid_num = G
+            e.map_range = G * ffmp_mod.MAP_RESOLUTION
+        e.is_collision(np.zeros((G, G), dtype=np.int32))
+        out["footprint"][str(G)] = [[int(c[0]), int(c[1])] for c in e.robot_grids]
+
+    # ---- is_collision: single-cell window maps at G in {64,100,128} ----
+    out["is_collision_single"] = {}
+    for G in (64, 100, 128):
+        e = FFMP()
+        if G != 100:
+            e.map_grid_num = G
+            e.map_range = G * ffmp_mod.MAP_RESOLUTION
+        c = G // 2
+        res = []
+        for i in range(c - 4, c + 5):
+            for j in range(c - 4, c + 5):
+                m = np.zeros((G, G), dtype=np.int32)
+                m[i, j] = 255
+                res.append([i, j, bool(e.is_collision(m))])
+        out["is_collision_single"][str(G)] = res
+
+    # ---- is_collision: random sparse maps at G=100 (2-D and (G,G,1) layouts) ----
+    e = FFMP()
+    rmaps, rres = [], []
+    for k in range(48):
+        dens = [0.0005, 0.002, 0.01, 0.05][k % 4]
+        m = (rng.random((100, 100)) < dens).astype(np.int32) * rng.integers(1, 256, (100, 100))
+        if k % 6 == 0:  # force a hit right on a footprint boundary cell
+            m[50 + 2, 50 + 1] = 7
+        rmaps.append(m.astype(np.uint8))
+        r2d = bool(e.is_collision(m.astype(np.int32)))
+        r3d = bool(e.is_collision(m.astype(np.int32)[:, :, None]))
+        rres.append([r2d, r3d])
+    maps["is_collision_maps"] = np.stack(rmaps)
+    out["is_collision_random"] = rres
+
+    # ---- is_collision2 on scan lists ----
+    f13 = float(np.float32(0.13))
+    f13_up = float(np.nextafter(np.float32(0.13), np.float32(1)))
+    hand = [
+        [None], [None, 0.5, 1.0], [None, 0.13], [None, f13], [None, f13_up],
+        [None, 0.0, 0.0, 0.2], [None, 0.0, 0.12], [0.12999999999999998], [0.13000000000000003],
+        [None, float("inf"), 0.3], [None, float("-inf")], [None, float("nan"), 0.2],
+        [], [None, 0.05, 0.01],
+    ]
+    scans = []
+    for s in hand:
+        with contextlib.redirect_stdout(io.StringIO()) as buf:
+            r = bool(e.is_collision2(s))
+        scans.append({"scan": s, "collide": r, "printed": buf.getvalue()})
+    for k in range(40):
+        L = [180, 360][k % 2]
+        v = rng.uniform(0.125, 6.0, L).astype(np.float32)
+        if k % 3 == 0:
+            v[rng.integers(0, L)] = np.float32(rng.choice([0.13, 0.1299, 0.1301, 0.12999999]))
+        if k % 5 == 0:
+            v[rng.integers(0, L, 4)] = 0.0
+        s = [None] + [float(x) for x in v]
+        with contextlib.redirect_stdout(io.StringIO()):
+            r = bool(e.is_collision2(s))
+        scans.append({"scan": s, "collide": r})
+    out["is_collision2"] = scans
+
+    # ---- is_goal ----
+    gv = [0.0, 0.49999999999999994, 0.5, 0.5000000000000001, 1.0, -1.0, 0.25]
+    gv += [float(x) for x in rng.uniform(0.3, 0.7, 40)]
+    out["is_goal"] = [[d, bool(e.is_goal(d))] for d in gv]
+
+    # ---- is_done ----
+    out["is_done"] = [[a, b, bool(e.is_done(a, b))] for a in (False, True) for b in (False, True)]
+
+    # ---- reward_calculator episode sequences (module-global d0) ----
+    seqs = []
+    for k in range(30):
+        steps = []
+        n = int(rng.integers(2, 12))
+        d = float(rng.uniform(1.0, 6.0))
+        for t in range(n):
+            first = t == 0
+            col = bool(rng.random() < 0.1)
+            goal = bool(rng.random() < 0.1)
+            orient = float(rng.uniform(-math.pi, math.pi))
+            rg = np.array([d, orient])
+            r = e.reward_calculator(rg, col, goal, first)
+            steps.append({"rel_goal": [d, orient], "col": col, "goal": goal, "first": first,
+                          "reward": float(r), "rtype": type(r).__name__})
+            d = float(max(0.0, d + rng.uniform(-0.1, 0.08)))
+        seqs.append(steps)
+    out["reward_sequences"] = seqs
+    # cross-instance leak of the module global
+    a, b = FFMP(), FFMP()
+    a.reward_calculator(np.array([3.0, 0.0]), False, False, True)
+    leak = b.reward_calculator(np.array([2.5, 0.0]), False, False, False)
+    out["reward_global_leak"] = {"d0_from_other_instance": 3.0, "d": 2.5, "reward": float(leak)}
+
+    # ---- rewarder (map) and rewarder2 (scan) composites ----
+    rw = []
+    for k in range(24):
+        m = maps["is_collision_maps"][k].astype(np.int32)
+        rg = np.array([float(rng.uniform(0.2, 4.0)), float(rng.uniform(-3, 3))])
+        first = (k % 4 == 0)
+        r, done = e.rewarder(m, rg, first)
+        rw.append({"map_index": k, "rel_goal": rg.tolist(), "first": first, "reward": float(r), "done": bool(done)})
+    out["rewarder"] = rw
+    rw2 = []
+    for k in range(24):
+        s = scans[(k * 3) % len(scans)]["scan"]
+        rg = np.array([float(rng.uniform(0.2, 4.0)), float(rng.uniform(-3, 3))])
+        first = (k % 4 == 0)
+        with contextlib.redirect_stdout(io.StringIO()):
+            r, done, goal = e.rewarder2(s, rg, first)
+        rw2.append({"scan_index": (k * 3) % len(scans), "rel_goal": rg.tolist(), "first": first,
+                    "reward": float(r), "done": bool(done), "is_goal": bool(goal)})
+    out["rewarder2"] = rw2
+
+    # ---- train.py helpers ----
+    h = _train_helpers()
+    ros = types.SimpleNamespace()
+    ros.pi_to_pi = types.MethodType(h["pi_to_pi"], ros)
+    angles = [0.0, math.pi, -math.pi, 3 * math.pi, -3 * math.pi, 2 * math.pi, -2 * math.pi, 7.0, -7.0,
+              math.pi - 1e-15, -math.pi + 1e-15, 1e-300, -1e-300, 4.0, -4.0]
+    angles += [float(x) for x in np.linspace(-20.0, 20.0, 161)]
+    angles += [float(x) for x in rng.uniform(-12.0, 12.0, 100)]
+    out["pi_to_pi"] = [[a, ros.pi_to_pi(a)] for a in angles]
+
+    ros.global_goal = types.SimpleNamespace(position=types.SimpleNamespace(x=0.0, y=0.0))
+    ros.relative_goal_calculator = types.MethodType(h["relative_goal_calculator"], ros)
+    rel = []
+    for k in range(120):
+        gx, gy = (float(v) for v in rng.uniform(-12, 12, 2))
+        px, py = (float(v) for v in rng.uniform(-12, 12, 2))
+        yaw = float(rng.uniform(-math.pi, math.pi))
+        if k < 4:
+            gx, gy, px, py = [(1.0, 0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 0.0), (-1.0, 0.0, 0.0, 0.0), (0.0, -2.0, 0.0, 0.0)][k]
+        ros.global_goal.position.x, ros.global_goal.position.y = gx, gy
+        r = ros.relative_goal_calculator(_Pose(px, py, yaw))
+        rel.append({"goal": [gx, gy], "pose": [px, py, yaw], "out": [float(r[0]), float(r[1])]})
+    out["relative_goal"] = rel
+
+    ros.pre_robot_pose = _Pose(0.0, 0.0, 0.0)
+    ros.robot_velocity_calculator = types.MethodType(h["robot_velocity_calculator"], ros)
+    vel = []
+    x, y, yaw = 0.0, 0.0, 0.0
+    for k in range(80):
+        first = (k % 10 == 0)
+        if first:
+            x, y, yaw = (float(v) for v in rng.uniform(-3, 3, 3))
+        else:
+            x += float(rng.uniform(-0.06, 0.06))
+            y += float(rng.uniform(-0.06, 0.06))
+            yaw = float(ros.pi_to_pi(yaw + float(rng.uniform(-0.6, 0.6))))
+        r = ros.robot_velocity_calculator(_Pose(x, y, yaw), first)
+        vel.append({"pose": [x, y, yaw], "first": first, "out": [float(r[0]), float(r[1])]})
+    out["velocity"] = vel
+
+    import torch
+    tenv = types.SimpleNamespace(map_memory=[])
+    tenv.make_temporal_maps = types.MethodType(h["make_temporal_maps"], tenv)
+    tm = []
+    for k in range(7):
+        first = k in (0, 4)
+        frame = torch.full((1, 3, 3), float(k))
+        with contextlib.redirect_stdout(io.StringIO()):
+            st = tenv.make_temporal_maps(frame, first)
+        tm.append({"frame_value": float(k), "first": first, "stack": st[:, 0, 0].tolist(), "shape": list(st.shape)})
+    out["temporal_maps"] = tm
+
+    with open(os.path.join(OUT_DIR, "ref_pinned.json"), "w") as f:
+        json.dump(out, f, indent=0, allow_nan=True)
+    np.savez_compressed(os.path.join(OUT_DIR, "ref_maps.npz"), **maps)
+    print("wrote", os.path.join(OUT_DIR, "ref_pinned.json"), "and ref_maps.npz")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""Helpers shared by the GPU parity tests and tests/parity_report.py."""
+from __future__ import annotations
+
+import numpy as np
+
+# Tolerances (north star: integer grid/obstacle indices bit-exact, float robot state <= 1e-5 abs).
+EXACT_FIELDS = ("state_m", "done", "is_goal", "collision", "truncated", "t", "episode")
+F64_STATE_ATOL = 1e-9      # pose / goal / obstacles / d0 (float64 state; 1e-5 is the contract)
+F32_OBS_ATOL = 1e-5        # state_g, state_v, state_t, grad, reward, lidar (float32 obs)
+POT_RTOL, POT_ATOL = 1e-6, 1e-5
+
+
+def gpu_snapshot(env, sl=slice(None)):
+    d = {k: getattr(env, k)[sl].detach().cpu().numpy() for k in
+         ("state_m", "state_g", "state_v", "state_t", "grad", "reward", "done", "is_goal", "collision",
+          "truncated", "pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record")}
+    d["potential"] = env.potential[sl].detach().cpu().numpy() if env.potential is not None else None
+    d["lidar"] = env.lidar[sl].detach().cpu().numpy() if env.lidar is not None else None
+    K = env.cfg.n_obst
+    if K == 0:
+        d["obst"] = d["obst"][:, :0]
+        d["obst_r"] = d["obst_r"][:, :0]
+    return d
+
+
+def oracle_snapshot(ref):
+    d = {k: getattr(ref, k) for k in
+         ("state_m", "state_g", "state_v", "state_t", "grad", "reward", "done", "is_goal", "collision",
+          "truncated", "pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record")}
+    d["potential"] = ref.potential if ref.with_potential else None
+    d["lidar"] = ref.lidar if ref.cfg.n_beams else None
+    return d
+
+
+def compare(g, o, where=""):
+    """Return a list of human-readable mismatch descriptions (empty == parity)."""
+    bad = []
+
+    def diff_count(a, b):
+        a = np.asarray(a)
+        b = np.asarray(b)
+        if a.shape != b.shape:
+            return f"shape {a.shape} vs {b.shape}"
+        ne = ~((a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b))
+        return int(ne.sum())
+
+    for k in EXACT_FIELDS + ("record",):
+        c = diff_count(g[k], o[k])
+        if c:
+            bad.append(f"{where} {k}: {c} elements differ")
+    for k in ("pose", "goal", "d0", "obst", "obst_r"):
+        a, b = np.asarray(g[k], dtype=np.float64), np.asarray(o[k], dtype=np.float64)
+        if a.shape != b.shape or not np.allclose(a, b, rtol=0, atol=F64_STATE_ATOL):
+            bad.append(f"{where} {k}: max |diff| {np.max(np.abs(a - b)) if a.shape == b.shape else 'shape'}")
+    for k in ("state_g", "state_v", "state_t", "grad", "reward", "lidar"):
+        if g[k] is None and o[k] is None:
+            continue
+        a, b = np.asarray(g[k], dtype=np.float64), np.asarray(o[k], dtype=np.float64)
+        same_inf = (np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b)))
+        fa = np.where(same_inf, 0.0, a)
+        fb = np.where(same_inf, 0.0, b)
+        if a.shape != b.shape or not np.allclose(fa, fb, rtol=0, atol=F32_OBS_ATOL):
+            m = np.max(np.abs(fa - fb)) if a.shape == b.shape else "shape"
+            bad.append(f"{where} {k}: max |diff| {m}")
+    if g["potential"] is not None:
+        a, b = g["potential"], o["potential"]
+        if not np.allclose(a, b, rtol=POT_RTOL, atol=POT_ATOL):
+            bad.append(f"{where} potential: max |diff| {np.max(np.abs(a - b))}")
+    return bad
+
+
+def exact_report(g, o):
+    """Count of non-bit-identical elements per float field (informational)."""
+    out = {}
+    for k in ("state_g", "state_v", "state_t", "grad", "reward", "lidar", "potential", "pose", "goal", "d0",
+              "obst", "record"):
+        if g.get(k) is None:
+            continue
+        a, b = np.asarray(g[k]), np.asarray(o[k])
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        out[k] = int((~same).sum())
+    return out

@@ -1,0 +1,145 @@
+"""Host logic and the C ABI without a GPU: the library loads, exports every symbol
+include/ffmp.h declares, its struct layout matches the ctypes binding, and the
+host-side entry points / argument validation behave (no kernel is launched)."""
+import ctypes as C
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+from flow_field_based_motion_planner_amd import _abi
+from flow_field_based_motion_planner_amd.config import (PRESETS, FFMPConfig, beam_table, bytes_per_env_step,
+                                                        footprint_offsets, preset)
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ffmp.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ffmp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_symbols_exported(lib):
+    names = header_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_abi._SIGS), "ctypes binding must cover exactly the header's entry points"
+
+
+def test_layout_and_version(lib):
+    assert lib.ffmp_abi_version() == _abi.ABI_VERSION
+    _abi.verify_layout(lib)
+
+
+@pytest.mark.parametrize("G", [8, 64, 100, 128, 256, 512])
+def test_footprint_lib_equals_host(lib, G):
+    assert _abi.footprint_from_lib(G, 0.05, 0.13) == footprint_offsets(G)
+
+
+def test_footprint_other_radii(lib):
+    for r in (0.0, 0.05, 0.2, 0.31):
+        assert _abi.footprint_from_lib(128, 0.05, r) == footprint_offsets(128, 0.05, r)
+
+
+def _null_structs():
+    return _abi.StateT(), _abi.ObsT(), _abi.OutT()
+
+
+def test_argument_validation_no_gpu(lib):
+    cfg = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=0))
+    st, ob, out = _null_structs()
+    rc = lib.ffmp_step(C.byref(cfg), 4, 0, None, C.byref(st), C.byref(ob), C.byref(out), None)
+    assert rc == -1 and b"NULL" in lib.ffmp_last_error()
+    bad = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=0))
+    bad.grid = 66
+    assert lib.ffmp_raster(C.byref(bad), 1, None, None, C.byref(ob), None) == -3
+    assert b"multiple of 4" in lib.ffmp_last_error()
+    bad.grid = 64
+    bad.n_obst = 65
+    assert lib.ffmp_raster(C.byref(bad), 1, None, None, C.byref(ob), None) == -3
+    lidar_cfg = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=8))  # beam_cs NULL
+    assert lib.ffmp_reset(C.byref(lidar_cfg), 1, 0, None, 1, C.byref(st), C.byref(ob), None) == -3
+    assert lib.ffmp_scan_collision(-1, 4, None, 0.13, None, None, None) == -1
+    # n == 0 with valid pointers is a no-op success (no launch)
+    dummy = (C.c_double * 8)()
+    p = C.cast(dummy, C.c_void_p).value
+    st2 = _abi.StateT(p, p, p, p, p, p, p, p, p)
+    ob2 = _abi.ObsT(p, p, p, p, p, p, p)
+    out2 = _abi.OutT(p, p, p, p, p)
+    assert lib.ffmp_step_state(C.byref(cfg), 0, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), None) == 0
+    assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == 0
+
+
+def test_config_validation():
+    with pytest.raises(ValueError):
+        FFMPConfig(grid=66)
+    with pytest.raises(ValueError):
+        FFMPConfig(n_obst=65)
+    with pytest.raises(ValueError):
+        FFMPConfig(n_beams=2000)
+    c = FFMPConfig(grid=256, n_beams=0)
+    assert c.mode == 1 and FFMPConfig(grid=256).mode == 3
+    assert c.W == 256 * 0.05 and c.lidar_range == 128 * 0.05
+
+
+def test_f32_constants_exact():
+    c = preset("C3")
+    f = c.f32_constants()
+    assert f["half_f"] == np.float32(0.5 * (256 * 0.05))
+    # cell G/2 is the robot centre exactly (ego coordinate 0)
+    assert np.float32(128) * f["res_f"] - f["half_f"] == 0.0
+    for G in (64, 100, 128, 256, 512):
+        ff = FFMPConfig(grid=G).f32_constants()
+        assert np.float32(G // 2) * ff["res_f"] - ff["half_f"] == 0.0, G
+    cc = _abi.make_cfg(c)
+    for k, v in f.items():
+        assert np.float32(getattr(cc, k)) == v
+
+
+def test_presets_match_baseline():
+    import json
+    with open(os.path.join(os.path.dirname(HEADER), "..", "BASELINE.json")) as fh:
+        cfgs = json.load(fh)["configs"]
+    assert len(cfgs) == 5
+    for name, txt in zip(("C1", "C2", "C3", "C4", "C5"), cfgs):
+        p = PRESETS[name]
+        c = preset(name)
+        assert f"{c.grid}×{c.grid}" in txt
+        assert f"{c.n_obst} " in txt
+        if name != "C1":
+            assert f"{p['n_envs']}" in txt.replace(",", "")
+        if c.n_beams and name != "C4":
+            assert f"{c.n_beams}-beam" in txt
+
+
+def test_beam_table():
+    t = beam_table(180)
+    assert t.shape == (180, 2)
+    assert t[0, 0] == math.cos(-math.pi) and t[0, 1] == math.sin(-math.pi)
+    assert np.allclose(np.hypot(t[:, 0], t[:, 1]), 1.0)
+
+
+def test_bytes_model():
+    b = bytes_per_env_step(preset("C3"))
+    assert b["raster"] == 12 * 256 * 256 + 4 * (16 + 8 * 16)
+    assert b["total"] > b["raster"]
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(_abi.FFMPBackendError):
+        _abi.load(str(tmp_path / "nope.so"))
+
+
+def test_product_never_imports_oracle():
+    root = os.path.join(os.path.dirname(HEADER), "..", "flow_field_based_motion_planner_amd")
+    for dp, _, files in os.walk(root):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', "").split("import")[0] or \
+                    not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f

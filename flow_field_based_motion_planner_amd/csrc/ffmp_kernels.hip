@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stddef.h>
 #include <string.h>
@@ -62,6 +63,29 @@ int check_cfg(const ffmp_cfg_t* c) {
       return fail(FFMP_E_CFG, "footprint cell outside the grid (index %d)", f);
   }
   return FFMP_OK;
+}
+
+// Raster launch shape.  Defaults are the measured best on MI355X
+// (profiles/r01_raster_tuning.txt): 4096 cells per block; plain stores for
+// planes of more than 16K cells (C3/C5: +1-2.5 %), nontemporal below (C2:
+// +1-3 %).  FFMP_RASTER_CPB (multiple of 1024) and FFMP_RASTER_NT (0/1)
+// override them for tuning sweeps only.
+struct RasterTuning {
+  int cells_per_block = 4096;
+  int nontemporal = -1;  // -1: by plane size
+};
+
+const RasterTuning& raster_tuning() {
+  static const RasterTuning t = [] {
+    RasterTuning r;
+    if (const char* v = getenv("FFMP_RASTER_CPB")) {
+      const int c = atoi(v);
+      if (c >= 1024 && c % 1024 == 0) r.cells_per_block = c;
+    }
+    if (const char* v = getenv("FFMP_RASTER_NT")) r.nontemporal = atoi(v) != 0 ? 1 : 0;
+    return r;
+  }();
+  return t;
 }
 
 constexpr int kEnvMode_Step = 0;
@@ -281,24 +305,22 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
 // raster_kernel: the HBM-bound hot path.
 //   block = 256 threads (4 waves); a pass covers 1024 consecutive cells of one
 //   env plane (each wave a contiguous 256-cell chunk, each lane 4 cells = one
-//   16-B store per plane).  Obstacles of both frames sit in LDS; per chunk a
-//   wave-uniform bitmask keeps only those whose disc (occupancy) or repulsive
-//   reach (potential) can touch the chunk's ego bounding box, and the world
-//   wall test is skipped when the chunk's four corners are safely inside.
+//   16-B store per plane).  Obstacles of both frames sit in LDS and lane k keeps
+//   obstacle k in registers; per chunk the cull is lane-parallel (lane k tests
+//   obstacle k against the chunk's ego bounding box, one __ballot builds the
+//   wave-uniform mask), and lanes 0..7 test the chunk corners against the world
+//   walls the same way, so the per-cell wall test runs only near a wall.
 // ============================================================================
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-FFMP_DEV void store_nt(float* p, float a, float b, float c, float d) {
+template <bool NT>
+FFMP_DEV void store4(float* p, float a, float b, float c, float d) {
   f32x4 v = {a, b, c, d};
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  else *reinterpret_cast<f32x4*>(p) = v;
 }
-
-struct ChunkCull {
-  uint64_t mask;
-  bool walls;  // per-cell wall test needed
-};
 
 FFMP_DEV float box_dist2(float px, float py, float x0, float x1, float y0, float y1) {
   const float dx = fmaxf(fmaxf(x0 - px, px - x1), 0.0f);
@@ -313,23 +335,13 @@ FFMP_DEV bool corner_inside(const ffmp_cfg_t& cfg, const FrameHdr& h, float ex, 
   return (fabsf(wx) <= W) && (fabsf(wy) <= W);
 }
 
-FFMP_DEV ChunkCull cull_chunk(const ffmp_cfg_t& cfg, const FrameHdr& h, const float4* obs, int K,
-                              float reach_extra, float x0, float x1, float y0, float y1) {
-  ChunkCull cc;
-  uint64_t m = 0;
-  for (int k = 0; k < K; ++k) {
-    const float4 o = obs[k];
-    const float reach = o.w + reach_extra;
-    if (box_dist2(o.x, o.y, x0, x1, y0, y1) <= reach * reach) m |= (1ull << k);
-  }
-  cc.mask = m;
-  cc.walls = !(corner_inside(cfg, h, x0, y0) && corner_inside(cfg, h, x0, y1) &&
-               corner_inside(cfg, h, x1, y0) && corner_inside(cfg, h, x1, y1));
-  return cc;
-}
+// r / G for 0 <= r < 256 + G (8 <= G <= 4096): (r + 0.5) / G is >= 0.5/G away
+// from an integer, far more than the float32 error of the product.
+FFMP_DEV int small_div(int r, float invG) { return (int)(((float)r + 0.5f) * invG); }
 
 }  // namespace
 
+template <bool NT>
 __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
@@ -361,35 +373,52 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const FrameHdr hp{s_hdr[4], s_hdr[5], s_hdr[6], s_hdr[7]};
   const float gx = s_hdr[8], gy = s_hdr[9];
   const float res = cfg.res_f, half = cfg.half_f;
-  const float pot_reach = cfg.rho0_f + cfg.cull_margin_f;
+  const float invG = 1.0f / (float)G;
+
+  const int wave = tid >> 6, lane = tid & 63;
+  // lane k's obstacle (cull operand) and its squared reach
+  const bool has = lane < K;
+  const float4 oc = has ? s_cur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 op = has ? s_prev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float rc = oc.w + cfg.rho0_f + cfg.cull_margin_f;  // potential reach (covers occupancy)
+  const float rp = op.w + cfg.cull_margin_f;               // occupancy reach
+  const float rc2 = rc * rc, rp2 = rp * rp;
+  // lanes 0..3: corners of the current frame, 4..7: previous frame
+  const FrameHdr hq = (lane < 4) ? hc : hp;
 
   float* m0 = state_m + (int64_t)e * 2 * G2;
   float* m1 = m0 + G2;
   float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
 
-  const int wave = tid >> 6, lane = tid & 63;
   const int qbeg = tile * cells_per_block;
   const int qend = min(qbeg + cells_per_block, G2);
 
   for (int q0 = qbeg + wave * 256; q0 < qend; q0 += 1024) {
-    // ---- wave chunk [q0, qlast] -> ego bounding box ----
+    // ---- wave chunk [q0, qlast] -> ego bounding box (wave-uniform) ----
     const int qlast = min(q0 + 255, G2 - 1);
-    const int i0 = q0 / G, i1 = qlast / G;
+    const int i0 = q0 / G;
+    const int r0 = q0 - i0 * G;
+    const int i1 = i0 + small_div(r0 + (qlast - q0), invG);
     int j0 = 0, j1 = G - 1;
-    if (i0 == i1) { j0 = q0 - i0 * G; j1 = qlast - i0 * G; }
+    if (i0 == i1) { j0 = r0; j1 = r0 + (qlast - q0); }
     const float bx0 = (float)i0 * res - half, bx1 = (float)i1 * res - half;
     const float by0 = (float)j0 * res - half, by1 = (float)j1 * res - half;
-    const ChunkCull cc = cull_chunk(cfg, hc, s_cur, K, pot_reach, bx0, bx1, by0, by1);
-    const ChunkCull cp = cull_chunk(cfg, hp, s_prev, K, cfg.cull_margin_f, bx0, bx1, by0, by1);
-    const uint64_t mc = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc.mask >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cc.mask);
-    const uint64_t mp = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cp.mask >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cp.mask);
 
+    // ---- lane-parallel cull ----
+    const uint64_t mc = __ballot(has && box_dist2(oc.x, oc.y, bx0, bx1, by0, by1) <= rc2);
+    const uint64_t mp = __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2);
+    const uint64_t wb = __ballot(lane >= 8 || corner_inside(cfg, hq, (lane & 1) ? bx1 : bx0,
+                                                             (lane & 2) ? by1 : by0));
+    const bool walls_c = (wb & 0xFull) != 0xFull;
+    const bool walls_p = (wb & 0xF0ull) != 0xF0ull;
+
+    // ---- this lane's 4 cells ----
+    const int off = r0 + lane * 4;
     const int q = q0 + lane * 4;
     if (q >= qend) continue;
-    const int i = q / G;
-    const int j = q - i * G;
+    const int di = small_div(off, invG);
+    const int i = i0 + di;
+    const int j = off - di * G;
     const float ex = (float)i * res - half;
     float ey[4];
 #pragma unroll
@@ -398,8 +427,8 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
     float occp[4], occc[4], U[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      occp[u] = (cp.walls && outside_world(cfg, hp, ex, ey[u])) ? 1.0f : 0.0f;
-      occc[u] = (cc.walls && outside_world(cfg, hc, ex, ey[u])) ? 1.0f : 0.0f;
+      occp[u] = (walls_p && outside_world(cfg, hp, ex, ey[u])) ? 1.0f : 0.0f;
+      occc[u] = (walls_c && outside_world(cfg, hc, ex, ey[u])) ? 1.0f : 0.0f;
       U[u] = attractive(cfg, ex, ey[u], gx, gy);
     }
     for (uint64_t m = mp; m; m &= m - 1) {
@@ -415,9 +444,9 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
         U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
       }
     }
-    store_nt(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
-    store_nt(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
-    if (pp) store_nt(pp + q, U[0], U[1], U[2], U[3]);
+    store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
+    store4<NT>(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
+    if (pp) store4<NT>(pp + q, U[0], U[1], U[2], U[3]);
   }
 }
 
@@ -600,12 +629,19 @@ int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uin
   if (!record || !obs || !obs->state_m) return fail(FFMP_E_ARG, "record/obs/state_m is NULL");
   if (n == 0) return FFMP_OK;
   const int G2 = cfg->grid * cfg->grid;
-  const int cpb = G2 < 8192 ? ((G2 + 1023) / 1024) * 1024 : 8192;
+  const RasterTuning& tu = raster_tuning();
+  const int cpb_max = tu.cells_per_block;
+  const int cpb = G2 < cpb_max ? ((G2 + 1023) / 1024) * 1024 : cpb_max;
   const int bpe = (G2 + cpb - 1) / cpb;
   const int64_t blocks = n * bpe;
   if (blocks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many raster blocks: %lld", (long long)blocks);
-  hipLaunchKernelGGL(raster_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
-                     bpe, cpb, record, mask, obs->state_m, obs->potential);
+  const bool nt = tu.nontemporal < 0 ? (G2 <= 16384) : (tu.nontemporal != 0);
+  if (nt)
+    hipLaunchKernelGGL(raster_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
+                       bpe, cpb, record, mask, obs->state_m, obs->potential);
+  else
+    hipLaunchKernelGGL(raster_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
+                       bpe, cpb, record, mask, obs->state_m, obs->potential);
   return check_launch("ffmp_raster");
 }
 

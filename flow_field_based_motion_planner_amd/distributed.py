@@ -1,0 +1,81 @@
+"""Env-batch sharding over one process per GPU.
+
+Envs are independent units: rank r owns the contiguous global range
+[offset_r, offset_r + count_r) and steps it with no per-step collective.  The
+global env index is part of every Philox key, so a trajectory does not depend
+on how the batch is sharded.  The only collective is the optional
+`gather_rollout`, an all-gather of per-env rollout scalars (reward f32, done /
+is_goal bytes) — over RCCL (`backend="nccl"` on ROCm, xGMI) for GPU ranks,
+gloo for CPU tests.  Observation planes are never gathered.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """(offset, count) of `rank`'s contiguous share; the first total % world ranks get one more."""
+    if world <= 0 or not 0 <= rank < world or total < 0:
+        raise ValueError("bad shard request")
+    base, extra = divmod(total, world)
+    count = base + (1 if rank < extra else 0)
+    offset = rank * base + min(rank, extra)
+    return offset, count
+
+
+def env_ranks() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment (defaults 0, 1, 0)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: Optional[str] = None, device: Optional[torch.device] = None) -> Tuple[int, int, int]:
+    """Initialise the default process group if WORLD_SIZE > 1 (nccl == RCCL for GPU ranks)."""
+    rank, world, local = env_ranks()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+        dist.init_process_group(backend, **kw)
+    return rank, world, local
+
+
+def _all_gather(t: torch.Tensor, group=None) -> torch.Tensor:
+    world = dist.get_world_size(group)
+    if t.is_cuda:
+        out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+        return out
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t.contiguous(), group=group)
+    return torch.cat(parts)
+
+
+def gather_rollout(reward: torch.Tensor, done: torch.Tensor, is_goal: torch.Tensor,
+                   total: Optional[int] = None, group=None) -> Dict[str, torch.Tensor]:
+    """All-gather per-env rollout scalars into global env order (one collective per call).
+
+    Shards may differ in size by one (shard_range); they are padded to the
+    largest shard for the collective and unpadded afterwards.  `total` is the
+    global env count (default: world * local count).
+    """
+    world = dist.get_world_size(group)
+    n = reward.shape[0]
+    if total is None:
+        total = n * world
+    cap = -(-total // world)
+    packed = torch.zeros(cap, 2, dtype=torch.float32, device=reward.device)
+    packed[:n, 0] = reward.float()
+    packed[:n, 1] = done.to(torch.float32) + 2.0 * is_goal.to(torch.float32)
+    allp = _all_gather(packed, group).view(world, cap, 2)
+    rows = []
+    for r in range(world):
+        _, cnt = shard_range(total, world, r)
+        rows.append(allp[r, :cnt])
+    g = torch.cat(rows)
+    flags = g[:, 1].to(torch.int32)
+    return {"reward": g[:, 0].contiguous(), "done": (flags & 1).bool(), "is_goal": (flags & 2).bool()}

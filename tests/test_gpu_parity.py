@@ -61,7 +61,7 @@ def test_step_parity(name):
 
 
 def test_truncation_and_autoreset_counts():
-    cfg = FFMPConfig(grid=32, n_obst=0, n_beams=0, max_steps=3, seed=9)
+    cfg = FFMPConfig(grid=64, n_obst=0, n_beams=0, max_steps=3, goal_min=1.2, goal_max=1.2, seed=9)
     env, ref, problems, counts = _run(cfg, 4, 7)
     assert not problems
     assert counts["trunc"] == 2 * 4  # steps 3 and 6

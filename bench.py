@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
 
 
@@ -93,16 +95,27 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     name = args.config
     pr = PRESETS[name]
     cfg = preset(name, seed=args.seed)
     strong = pr["gpus"] > 1
     n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
+    # a strong-scaling preset (C4/C5) on fewer GPUs than it is quoted on may not fit one
+    # GPU's HBM: then every rank runs the preset's per-GPU share instead (weak scaling)
+    per_env = 4 * cfg.grid * cfg.grid * (2 + (0 if args.no_potential else 1)) + 4096
+    budget = int(0.7 * torch.cuda.get_device_properties(dev).total_memory)
+    if not args.envs and strong and n * per_env > budget:
+        n = pr["n_envs"] // pr["gpus"]
+        strong = False
     n_total = n * world
     env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential)
 
@@ -130,7 +143,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
@@ -158,7 +171,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
-                       "potential": not args.no_potential, "parallelism": f"env-shard x{world}"},
+                       "potential": not args.no_potential, "parallelism": f"env-shard x{world}",
+                       "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,

@@ -98,11 +98,29 @@ _SIGS = {
 _LIB: Optional[C.CDLL] = None
 
 
+def _hip_runtimes_mapped():
+    """Distinct libamdhip64 files mapped into this process (Linux /proc/self/maps)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+    except OSError:  # pragma: no cover
+        return []
+
+
 def load(path: Optional[str] = None) -> C.CDLL:
-    """Load libffmp once; raise FFMPBackendError if it is missing."""
+    """Load libffmp once; raise FFMPBackendError if it is missing.
+
+    torch (ROCm wheel) ships its own libamdhip64 with the same soname as
+    /opt/rocm's.  Importing torch FIRST makes libffmp's libamdhip64.so.7 resolve
+    to torch's copy, so the process holds ONE HIP runtime (two runtimes in one
+    process cannot both open the GPU)."""
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
+    try:
+        import torch  # noqa: F401  (binds libamdhip64.so.7 to torch's runtime)
+    except ImportError:  # pragma: no cover - pure C users
+        pass
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise FFMPBackendError(
@@ -116,6 +134,10 @@ def load(path: Optional[str] = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    rts = _hip_runtimes_mapped()
+    if len(rts) > 1:
+        raise FFMPBackendError(f"two HIP runtimes are loaded in this process: {rts}; import torch before "
+                               "loading libffmp (flow_field_based_motion_planner_amd._abi.load does this)")
     if lib.ffmp_abi_version() != ABI_VERSION:
         raise FFMPBackendError(f"libffmp ABI {lib.ffmp_abi_version()} != expected {ABI_VERSION}")
     if path is None:

@@ -1,0 +1,193 @@
+"""The reference's FFMP methods (src/gym_ffmp/envs/ffmp.py:85-188), run through the
+HIP kernels of the drop-in FFMP class, against the golden vectors generated from
+the reference itself; plus the batched kernels on the same vectors in one launch,
+and the gym reset/step surface."""
+import contextlib
+import ctypes as C
+import io
+
+import numpy as np
+import pytest
+import torch
+
+import flow_field_based_motion_planner_amd as P
+from flow_field_based_motion_planner_amd import _abi, env as envmod
+from flow_field_based_motion_planner_amd.config import FFMPConfig
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def ffmp():
+    envmod._reset_global_d0()
+    return envmod.FFMP()
+
+
+def test_is_collision_single_cells(golden, ffmp):
+    for G in ("64", "100", "128"):
+        e = envmod.FFMP()
+        if G != "100":
+            e.map_grid_num = int(G)
+            e.map_range = int(G) * 0.05
+        for i, j, want in golden["is_collision_single"][G]:
+            m = np.zeros((int(G), int(G)), dtype=np.int32)
+            m[i, j] = 255
+            assert e.is_collision(m) == want, (G, i, j)
+    assert [tuple(c) for c in e.robot_grids] == [tuple(c) for c in golden["footprint"]["128"]]
+
+
+def test_is_collision_random_maps(golden, golden_maps, ffmp):
+    maps = golden_maps["is_collision_maps"].astype(np.int32)
+    for m, (w2d, w3d) in zip(maps, golden["is_collision_random"]):
+        assert ffmp.is_collision(m) == w2d
+        assert ffmp.is_collision(m[:, :, None]) == w3d
+
+
+def test_is_collision2_and_banner(golden, ffmp):
+    for case in golden["is_collision2"]:
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            got = ffmp.is_collision2(case["scan"])
+        assert got == case["collide"], case["scan"][:4]
+        if "printed" in case:
+            assert buf.getvalue() == case["printed"]
+
+
+def test_is_goal_is_done(golden, ffmp):
+    for d, want in golden["is_goal"]:
+        assert ffmp.is_goal(d) == want
+    for a, b, want in golden["is_done"]:
+        assert ffmp.is_done(a, b) == want
+
+
+def test_reward_sequences_module_global(golden, ffmp):
+    with pytest.raises(NameError):
+        ffmp.reward_calculator(np.array([1.0, 0.0]), False, False, False)
+    for seq in golden["reward_sequences"]:
+        for s in seq:
+            r = ffmp.reward_calculator(np.array(s["rel_goal"]), s["col"], s["goal"], s["first"])
+            assert r == s["reward"] and type(r).__name__ == s["rtype"], s
+    leak = golden["reward_global_leak"]
+    a, b = envmod.FFMP(), envmod.FFMP()
+    a.reward_calculator(np.array([leak["d0_from_other_instance"], 0.0]), False, False, True)
+    assert b.reward_calculator(np.array([leak["d"], 0.0]), False, False, False) == leak["reward"]
+
+
+def test_rewarder_and_rewarder2(golden, golden_maps, ffmp):
+    maps = golden_maps["is_collision_maps"].astype(np.int32)
+    for c in golden["rewarder"]:
+        r, done = ffmp.rewarder(maps[c["map_index"]], np.array(c["rel_goal"]), c["first"])
+        assert (r, done) == (c["reward"], c["done"])
+    scans = golden["is_collision2"]
+    for c in golden["rewarder2"]:
+        with contextlib.redirect_stdout(io.StringIO()):
+            r, done, g = ffmp.rewarder2(scans[c["scan_index"]]["scan"], np.array(c["rel_goal"]), c["first"])
+        assert (r, done, g) == (c["reward"], c["done"], c["is_goal"])
+
+
+def test_batched_kernels_on_golden(golden, golden_maps, lib):
+    """All golden scans / maps in ONE launch each (n > 1 batch path)."""
+    dev = torch.device("cuda:0")
+    scans = [c for c in golden["is_collision2"] if len(c["scan"]) > 0]
+    L = max(len(c["scan"]) for c in scans)
+    arr = np.zeros((len(scans), L))
+    for k, c in enumerate(scans):
+        arr[k, :len(c["scan"])] = [0.0 if v is None else v for v in c["scan"]]
+    t = torch.as_tensor(arr).to(dev)
+    col = torch.empty(len(scans), dtype=torch.uint8, device=dev)
+    mn = torch.empty(len(scans), dtype=torch.float64, device=dev)
+    _abi.check(lib.ffmp_scan_collision_f64(len(scans), L, t.data_ptr(), 0.13, col.data_ptr(), mn.data_ptr(), None))
+    assert col.cpu().numpy().astype(bool).tolist() == [c["collide"] for c in scans]
+    # float32 variant on float32-representable scans
+    f32 = [k for k, c in enumerate(scans) if all(v is None or float(np.float32(v)) == v for v in c["scan"])]
+    t32 = torch.as_tensor(arr[f32].astype(np.float32)).to(dev)
+    col32 = torch.empty(len(f32), dtype=torch.uint8, device=dev)
+    _abi.check(lib.ffmp_scan_collision(len(f32), L, t32.data_ptr(), 0.13, col32.data_ptr(), None, None))
+    assert col32.cpu().numpy().astype(bool).tolist() == [scans[k]["collide"] for k in f32]
+    # footprint over all random maps
+    maps = torch.as_tensor(golden_maps["is_collision_maps"].astype(np.float32)).to(dev)
+    cfg = _abi.make_cfg(FFMPConfig(grid=100, n_obst=0, n_beams=0))
+    fc = torch.empty(maps.shape[0], dtype=torch.uint8, device=dev)
+    _abi.check(lib.ffmp_footprint_collision(C.byref(cfg), maps.shape[0], maps.data_ptr(), 100 * 100,
+                                            fc.data_ptr(), None))
+    assert fc.cpu().numpy().astype(bool).tolist() == [w for w, _ in golden["is_collision_random"]]
+
+
+def test_gym_surface_reset_step():
+    e = envmod.FFMP(FFMPConfig(grid=100, n_obst=4, n_beams=180, autoreset=False, seed=3), verbose=False)
+    with pytest.raises(RuntimeError):
+        e.step(3)
+    obs = e.reset()
+    assert obs["local_map"].shape == (100, 100, 1) and obs["local_map"].dtype == np.int32
+    assert obs["relative_goal"].dtype == np.float32 and obs["velocity"].tolist() == [0.0, 0.0]
+    assert e.observation_space["local_map"].contains(obs["local_map"])
+    done = False
+    steps = 0
+    while not done:
+        obs, r, done, info = e.step(steps % 28)
+        steps += 1
+        assert isinstance(r, float)
+        assert info["state_m"].shape == (1, 2, 100, 100)
+    assert steps <= 200 and (info["truncated"] or info["collision"] or info["is_goal"])
+    with pytest.raises(RuntimeError):
+        e.step(0)
+    with pytest.raises(IndexError):
+        e.reset()
+        e.step(28)
+
+
+def test_gym_ffmp_alias_and_network_contract():
+    P.install_gym_ffmp_alias()
+    import gym_ffmp  # noqa: F401
+    from gym_ffmp.envs.ffmp import FFMP
+    from gym_ffmp.envs.robot.config import RobotAction
+    assert RobotAction().commander(27).linear_v == 0.6
+    v = P.FFMPVec(4, FFMPConfig(grid=100, n_obst=4, n_beams=180), device="cuda:0")
+    o = v.reset()
+    # the reference Network consumes state_m (B,2,100,100) and cat(state_g, state_v, state_t) (B,5)
+    assert tuple(o["state_m"].shape) == (4, 2, 100, 100) and o["state_m"].dtype == torch.float32
+    assert torch.cat((o["state_g"], o["state_v"], o["state_t"]), 1).shape == (4, 5)
+    assert isinstance(FFMP(), FFMP)
+
+
+def test_vec_api_mask_reset_errors_checkpoint():
+    cfg = FFMPConfig(grid=64, n_obst=8, n_beams=32, moving=True, autoreset=False, seed=5)
+    v = P.FFMPVec(6, cfg, device="cuda:0")
+    with pytest.raises(RuntimeError):
+        v.step(torch.zeros(6, dtype=torch.int64, device="cuda:0"))
+    v.reset()
+    ep0 = v.episode.clone()
+    mask = torch.tensor([1, 0, 0, 1, 0, 0], dtype=torch.bool, device="cuda:0")
+    keep_sm = v.state_m[1].clone()
+    v.reset(mask=mask)
+    assert v.episode.cpu().tolist() == [1, 0, 0, 1, 0, 0] and torch.equal(v.state_m[1], keep_sm)
+    assert int(ep0.sum()) == 0
+    # invalid action ids are run as action 3 and reported
+    v.step(torch.tensor([0, 1, 2, 3, 4, 99], device="cuda:0"))
+    with pytest.raises(ValueError):
+        v.check_errors()
+    v.check_errors()  # cleared
+    # checkpoint / resume reproduces the trajectory bit for bit
+    sd = v.state_dict()
+    acts = [torch.randint(0, 28, (6,), device="cuda:0") for _ in range(3)]
+    for a in acts:
+        v.step(a)
+    ref = v.state_m.clone(), v.pose.clone()
+    w = P.FFMPVec(6, cfg, device="cuda:0")
+    w.load_state_dict(sd)
+    for a in acts:
+        w.step(a)
+    assert torch.equal(w.state_m, ref[0]) and torch.equal(w.pose, ref[1])
+    # copies are decoupled from the env buffers
+    obs, r, d, info = v.step(acts[0], copy=True)
+    before = obs["state_m"].clone()
+    v.step(acts[1])
+    assert torch.equal(obs["state_m"], before)
+
+
+def test_no_potential_mode():
+    cfg = FFMPConfig(grid=64, n_obst=4, n_beams=0, seed=2)
+    v = P.FFMPVec(3, cfg, device="cuda:0", potential=False)
+    o = v.reset()
+    assert "potential" not in o and v.potential is None
+    v.step(torch.zeros(3, dtype=torch.int64, device="cuda:0"))

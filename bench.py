@@ -179,6 +179,7 @@ def main():
                          "kernel": "raster_kernel", "kernel_ms": raster_ms,
                          "algorithmic_bytes_per_launch": b["raster"] * n},
             "env_kernel_ms": state_ms,
+            "hbm_placement": env.placement,
             "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
         }
         if world == 1 and args.cpu_seconds > 0:

@@ -49,7 +49,8 @@ class FFMPVec:
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
-                 potential: bool = True, seed: Optional[int] = None):
+                 potential: bool = True, seed: Optional[int] = None, arena: bool = True,
+                 placement_check: bool = True):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -68,43 +69,130 @@ class FFMPVec:
             raise ValueError("num_envs must be positive")
         self.env_offset = int(env_offset)
         self.with_potential = bool(potential)
+        self.arena = bool(arena)
+        self.placement = {"tries": 0, "gbs": None, "all_gbs": []}
         self._alloc()
         self._build_structs()
+        if self.arena and placement_check and self._arena_buf.numel() >= self.PLACEMENT_MIN_BYTES:
+            self._place_arena()
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
-    def _alloc(self):
-        cfg, N, dev = self.cfg, self.num_envs, self.device
+    _ARENA_ALIGN = 2 << 20
+
+    def _buffer_specs(self):
+        """(name, shape, dtype) of every per-shard device buffer."""
+        cfg, N = self.cfg, self.num_envs
         G, K, L = cfg.grid, cfg.n_obst, cfg.n_beams
-        f32, f64 = torch.float32, torch.float64
-        e = lambda *s, dtype=f32: torch.empty(*s, dtype=dtype, device=dev)  # noqa: E731
-        z = lambda *s, dtype=f32: torch.zeros(*s, dtype=dtype, device=dev)  # noqa: E731
-        # state
-        self.pose = z(N, 3, dtype=f64)
-        self.goal = z(N, 2, dtype=f64)
-        self.d0 = z(N, dtype=f64)
-        self.obst = z(N, max(K, 1), 4, dtype=f64)
-        self.obst_r = z(N, max(K, 1), dtype=f64)
-        self.t = z(N, dtype=torch.int32)
-        self.episode = z(N, dtype=torch.int32)
-        self.record = z(N, cfg.record_len())
-        self.err = z(1, dtype=torch.int32)
-        # obs
-        self.state_m = e(N, 2, G, G)
-        self.state_g = z(N, 2)
-        self.state_v = z(N, 2)
-        self.state_t = z(N, 1)
-        self.potential = e(N, G, G) if self.with_potential else None
-        self.grad = z(N, 2)
-        self.lidar = z(N, L) if L > 0 else None
-        # outputs
-        self.reward = z(N)
-        self.done = z(N, dtype=torch.bool)
-        self.is_goal = z(N, dtype=torch.bool)
-        self.collision = z(N, dtype=torch.bool)
-        self.truncated = z(N, dtype=torch.bool)
-        # tables
-        self.beam_cs = torch.as_tensor(beam_table(L), dtype=f64).to(dev) if L > 0 else None
+        f32, f64, i32, b = torch.float32, torch.float64, torch.int32, torch.bool
+        specs = [
+            # observation planes first: the big, hot, write-streamed buffers
+            ("state_m", (N, 2, G, G), f32),
+            ("potential", (N, G, G), f32),
+            # state
+            ("pose", (N, 3), f64), ("goal", (N, 2), f64), ("d0", (N,), f64),
+            ("obst", (N, max(K, 1), 4), f64), ("obst_r", (N, max(K, 1)), f64),
+            ("t", (N,), i32), ("episode", (N,), i32), ("record", (N, cfg.record_len()), f32),
+            ("err", (1,), i32),
+            # small obs + outputs
+            ("state_g", (N, 2), f32), ("state_v", (N, 2), f32), ("state_t", (N, 1), f32),
+            ("grad", (N, 2), f32), ("lidar", (N, L), f32),
+            ("reward", (N,), f32), ("done", (N,), b), ("is_goal", (N,), b), ("collision", (N,), b),
+            ("truncated", (N,), b),
+        ]
+        if not self.with_potential:
+            specs = [sp for sp in specs if sp[0] != "potential"]
+        if L == 0:
+            specs = [sp for sp in specs if sp[0] != "lidar"]
+        return specs
+
+    def _alloc(self):
+        """All per-shard buffers, zero-initialised.  With arena=True (default) they are views
+        into ONE device allocation carved at 2 MiB boundaries.  Measured on MI355X
+        (profiles/r01_placement.txt): the raster's three concurrent store streams ran at
+        5.8 or 6.9 TB/s depending on how separately allocated planes happened to be placed
+        physically, and at the fast end every time when all planes lived in one allocation."""
+        dev = self.device
+        specs = self._buffer_specs()
+        self.potential = None
+        self.lidar = None
+        if self.arena:
+            offs, off = [], 0
+            for _, shape, dtype in specs:
+                off = -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN
+                offs.append(off)
+                n = 1
+                for d in shape:
+                    n *= d
+                off += n * torch.empty((), dtype=dtype).element_size()
+            self._arena_buf = torch.zeros(max(off, 1), dtype=torch.uint8, device=dev)
+            for (name, shape, dtype), o in zip(specs, offs):
+                n = 1
+                for d in shape:
+                    n *= d
+                nb = n * torch.empty((), dtype=dtype).element_size()
+                setattr(self, name, self._arena_buf[o:o + nb].view(dtype).view(shape))
+        else:
+            self._arena_buf = None
+            for name, shape, dtype in specs:
+                setattr(self, name, torch.zeros(shape, dtype=dtype, device=dev))
+        L = self.cfg.n_beams
+        self.beam_cs = torch.as_tensor(beam_table(L), dtype=torch.float64).to(dev) if L > 0 else None
+
+    # Placement check (see profiles/r01_placement.txt): the raster's store bandwidth is a
+    # property of the physical memory behind an allocation (measured 5.7-5.8 vs 6.8-7.0 TB/s
+    # for identical virtual layouts, persistent for the life of the allocation).  Time the
+    # raster kernel on the fresh arena; below PLACEMENT_GOOD_GBS, allocate another arena while
+    # still holding the first (so the allocator must hand out different memory) and keep the
+    # fastest of at most PLACEMENT_TRIES.
+    PLACEMENT_MIN_BYTES = 1 << 30
+    PLACEMENT_GOOD_GBS = 6400.0
+    PLACEMENT_TRIES = 4
+    PLACEMENT_SPACER = 3 << 30  # held between candidates so each comes from different memory
+
+    def _raster_gbs(self) -> float:
+        """Raster store bandwidth on the current buffers, measured on a real reset state
+        (a zeroed record would stack every disc on the robot cell: not representative)."""
+        from .config import bytes_per_env_step
+        self.reset()
+        with torch.cuda.device(self.device):
+            self.raster()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(2):
+                self.raster()
+            ev[1].record()
+            torch.cuda.synchronize(self.device)
+        ms = ev[0].elapsed_time(ev[1]) / 2
+        b = bytes_per_env_step(self.cfg, potential=self.with_potential)["raster"] * self.num_envs
+        return b / (ms * 1e-3) / 1e9
+
+    def _place_arena(self):
+        kept = []  # (gbs, arena tensor, buffers)
+        spacers = []
+        for k in range(self.PLACEMENT_TRIES):
+            if k:
+                spacers.append(torch.empty(self.PLACEMENT_SPACER * k, dtype=torch.uint8, device=self.device))
+                self._alloc()
+                self._build_structs()
+            gbs = self._raster_gbs()
+            self.placement["all_gbs"].append(round(gbs, 1))
+            kept.append((gbs, self._arena_buf, {n: getattr(self, n) for n, _, _ in self._buffer_specs()}))
+            if gbs >= self.PLACEMENT_GOOD_GBS:
+                break
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if free < 1.25 * self._arena_buf.numel() + self.PLACEMENT_SPACER * (k + 1):
+                break  # no room for another candidate arena
+        best = max(range(len(kept)), key=lambda i: kept[i][0])
+        gbs, buf, views = kept[best]
+        self._arena_buf = buf
+        for n, v in views.items():
+            setattr(self, n, v)
+        self._build_structs()
+        self.placement.update(tries=len(kept), gbs=round(gbs, 1))
+        del kept, spacers
+        torch.cuda.empty_cache()
+        self._arena_buf.zero_()
 
     def _build_structs(self):
         self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
@@ -219,6 +307,8 @@ class FFMPVec:
         self._needs_reset = False
 
     def hbm_bytes(self) -> int:
+        if self._arena_buf is not None:
+            return self._arena_buf.numel()
         return sum(t.numel() * t.element_size() for t in vars(self).values() if isinstance(t, torch.Tensor))
 
     def __repr__(self):

@@ -1,0 +1,37 @@
+"""A/B: raster store bandwidth with arena vs separate allocations, several fresh allocations
+each, in one process (same box).  Usage: python tools/alloc_ab.py [trials]"""
+import gc
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from flow_field_based_motion_planner_amd.config import bytes_per_env_step, preset  # noqa: E402
+from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
+
+trials = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+cfg = preset("C3")
+N = 32768
+b = bytes_per_env_step(cfg)["raster"] * N
+for t in range(trials):
+    for arena in (True, False):
+        env = FFMPVec(N, cfg, device="cuda:0", arena=arena, placement_check=arena)
+        env.reset()
+        a = torch.randint(0, 28, (N,), device="cuda:0")
+        for _ in range(3):
+            env.step(a)
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(20):
+            env.raster()
+        ev[1].record()
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / 20
+        print(f"trial {t} arena+check={arena}: raster {ms:.3f} ms  {b / ms / 1e6:.0f} GB/s  placement={env.placement}",
+              flush=True)
+        del env, a
+        gc.collect()
+        torch.cuda.empty_cache()

@@ -40,6 +40,28 @@ __global__ __launch_bounds__(256) void three_planes(float* __restrict__ sm, floa
   }
 }
 
+// P planes, each lane writes V consecutive float4 per plane per pass (V*16 B per lane).
+template <int P, int V, int BS>
+__global__ __launch_bounds__(BS) void multi_planes(float* __restrict__ base, long plane_stride, int G2, int bpe, int cpb) {
+  const long e = blockIdx.x / bpe;
+  const int tile = blockIdx.x - e * bpe;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qend = min((tile + 1) * cpb, G2);
+  constexpr int WAVES = BS / 64;
+  for (int q0 = tile * cpb + wave * 256 * V; q0 < qend; q0 += WAVES * 256 * V) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      float* dst = base + (long)p * plane_stride + e * (long)G2;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int q = q0 + (v * 64 + lane) * 4;
+        f32x4 a = {(float)q, (float)p, 1.f, 2.f};
+        *(f32x4*)(dst + q) = a;
+      }
+    }
+  }
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256) void flat(float* __restrict__ p, long n4) {
   long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -87,6 +109,43 @@ int main(int argc, char** argv) {
     float t1 = time_it([&] { hipLaunchKernelGGL(flat<true>, dim3(grid), dim3(256), 0, 0, sm, n4); });
     printf("flat grid=%d %.2f GB: plain %.0f GB/s | nt %.0f GB/s\n", grid, n4 * 16 / 1e9, n4 * 16 / t0 / 1e6,
            n4 * 16 / t1 / 1e6);
+  }
+  // vendor fill as a reference point
+  {
+    const size_t n32 = N * 2L * G2;
+    float t = time_it([&] { (void)hipMemsetD32Async((hipDeviceptr_t)sm, 0x3f800000, n32, 0); });
+    printf("hipMemsetD32Async %.2f GB: %.0f GB/s\n", n32 * 4 / 1e9, n32 * 4 / t / 1e6);
+  }
+  // plane-count / width / block-size variants on the same 3*N*G2 floats (as P planes of N*G2*3/P)
+  {
+    float* base = sm;  // reuse: sm has 2*N*G2, pot N*G2; treat as one 3*N*G2 region (contiguous? no) -> use sm only
+    (void)base;
+  }
+  {
+    float* big;
+    CHECK(hipMalloc(&big, N * 3L * G2 * 4));
+    const long ps = N * (long)G2;
+    auto run = [&](const char* name, auto kern, int P, int V, int BS) {
+      const int cpb = 4096;
+      const int bpe = (G2 + cpb - 1) / cpb;
+      const long planes_env = N * (long)bpe;
+      const long stride = ps * 3 / P;   // P planes of equal size covering the same bytes
+      const int G2eff = (int)(stride / N);
+      const int bpe2 = (G2eff + cpb - 1) / cpb;
+      (void)planes_env;
+      float t = time_it([&] { hipLaunchKernelGGL(kern, dim3(N * bpe2), dim3(BS), 0, 0, big, stride, G2eff, bpe2, cpb); });
+      printf("%-28s P=%d V=%d BS=%d: %.3f ms %.0f GB/s\n", name, P, V, BS, t, bytes / t / 1e6);
+    };
+    run("multi", multi_planes<3, 1, 256>, 3, 1, 256);
+    run("multi", multi_planes<3, 2, 256>, 3, 2, 256);
+    run("multi", multi_planes<3, 4, 256>, 3, 4, 256);
+    run("multi", multi_planes<3, 1, 512>, 3, 1, 512);
+    run("multi", multi_planes<3, 1, 1024>, 3, 1, 1024);
+    run("multi", multi_planes<1, 1, 256>, 1, 1, 256);
+    run("multi", multi_planes<1, 4, 256>, 1, 4, 256);
+    run("multi", multi_planes<6, 1, 256>, 6, 1, 256);
+    run("multi", multi_planes<12, 1, 256>, 12, 1, 256);
+    CHECK(hipFree(big));
   }
   CHECK(hipFree(sm));
   CHECK(hipFree(pot));

@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -117,28 +118,24 @@ def main():
         n = pr["n_envs"] // pr["gpus"]
         strong = False
     n_total = n * world
-    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential)
+    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline)
 
     K, W = args.steps, args.warmup
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
     env.reset()
     for w in range(W):
-        env.step_state(actions[w])
-        env.raster()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        env.step(actions[w])
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    raster_ev = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
-        e0, e1, e2 = evs[k]
-        e0.record()
-        env.step_state(actions[W + k])
-        e1.record()
-        env.raster()
-        e2.record()
+        evs[k][0].record()
+        env.step(actions[W + k], timing=raster_ev)
+        evs[k][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -149,11 +146,15 @@ def main():
     el = float(t.item())
     env.check_errors()
 
-    raster_ms = sum(evs[k][1].elapsed_time(evs[k][2]) for k in range(K)) / K
-    state_ms = sum(evs[k][0].elapsed_time(evs[k][1]) for k in range(K)) / K
+    # raster kernel: HIP events around every launch on the launch stream
+    r_ms = [a.elapsed_time(b) for a, b, _ in raster_ev]
+    r_envs = [m for _, _, m in raster_ev]
+    raster_ms = sum(r_ms) / len(r_ms)
+    step_ms_ev = sum(a.elapsed_time(b) for a, b in evs) / K
     b = bytes_per_env_step(cfg, potential=not args.no_potential)
-    achieved = b["raster"] * n / (raster_ms * 1e-3) / 1e9
-    traffic = load_traffic(name, n)
+    achieved = b["raster"] * sum(r_envs) / (sum(r_ms) * 1e-3) / 1e9
+    per_launch_envs = r_envs[0]
+    traffic = load_traffic(name, per_launch_envs)
 
     if rank == 0:
         out = {
@@ -177,9 +178,12 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
                          "kernel": "raster_kernel", "kernel_ms": raster_ms,
-                         "algorithmic_bytes_per_launch": b["raster"] * n},
-            "env_kernel_ms": state_ms,
-            "hbm_placement": env.placement,
+                         "algorithmic_bytes_per_launch": b["raster"] * per_launch_envs,
+                         "launches_per_step": len(r_ms) // K},
+            "raster_ms_per_step": sum(r_ms) / K,
+            "step_ms_events": step_ms_ev,
+            "pipeline_slices": env.pipeline_slices,
+            "raster_autotune": env.placement,
             "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
         }
         if world == 1 and args.cpu_seconds > 0:

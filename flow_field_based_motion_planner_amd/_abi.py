@@ -81,11 +81,13 @@ _SIGS = {
     "ffmp_abi_version": (C.c_int, []),
     "ffmp_last_error": (C.c_char_p, []),
     "ffmp_layout": (_I64, [_I32]),
+    "ffmp_set_tuning": (_I32, [_I32, _I32]),
     "ffmp_footprint": (C.c_int, [_I32, C.c_double, C.c_double, _P, _P, _I32]),
     "ffmp_reset": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, _I32, C.POINTER(StateT), C.POINTER(ObsT), _P]),
     "ffmp_step_state": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, C.POINTER(StateT), C.POINTER(ObsT),
                                   C.POINTER(OutT), _P]),
     "ffmp_raster": (C.c_int, [C.POINTER(CfgT), _I64, _P, _P, C.POINTER(ObsT), _P]),
+    "ffmp_raster_ex": (C.c_int, [C.POINTER(CfgT), _I64, _P, _P, C.POINTER(ObsT), _I32, _I32, _P]),
     "ffmp_step": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, C.POINTER(StateT), C.POINTER(ObsT),
                             C.POINTER(OutT), _P]),
     "ffmp_reward_done": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -162,6 +164,18 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
         got = lib.ffmp_layout(k)
         if got != v:
             raise FFMPBackendError(f"ABI layout mismatch (item {k}): library {got}, ctypes {v}")
+
+
+TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES = 1, 2, 3, 4
+RASTER_NT, RASTER_PLAIN, RASTER_XCD = 1, 2, 4
+
+
+def set_tuning(key: int, value: int) -> int:
+    """Process-wide launch-shape tuning (include/ffmp.h FFMP_TUNE_*); returns the previous value."""
+    prev = load().ffmp_set_tuning(int(key), int(value))
+    if prev < 0:
+        check(prev, "ffmp_set_tuning")
+    return prev
 
 
 def footprint_from_lib(grid: int, res: float, robot_r: float):

@@ -210,21 +210,54 @@ FFMP_DEV bool occupied_cell(const ffmp_cfg_t& cfg, const FrameHdr& h, const floa
   return o;
 }
 
-// One lidar beam (float64): nearest of the K discs and the 4 world walls.
-// Returns +inf for no return within lidar_max, -inf if the origin is inside a disc.
-FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, double x, double y, double c, double s,
-                           double bc, double bs, const double* ox, const double* oy,
-                           const double* orad, int K) {
+// ---- lidar ------------------------------------------------------------------
+// Per-env lidar scene, built lane-parallel once per env (lane k = disc k): the discs that
+// can return a hit within lidar_max or contain the sensor, whether the sensor is inside a
+// disc, and which walls are within range.  A disc whose surface is farther than
+// lidar_max + kLidarCullMargin can never produce an accepted hit (any ray's entry distance is
+// >= |rel| - r, and float64 rounding moves the computed value by < 3e-7 m), and likewise a
+// wall farther than that (|dir| <= 1), so skipping them leaves every range bit-identical.
+constexpr double kLidarCullMargin = 1e-6;
+
+struct LidarScene {
+  uint64_t mask;
+  bool inside;
+  bool wxp, wxn, wyp, wyn;
+};
+
+// Call from every lane of the env's wave; lane k < K holds disc k.
+FFMP_DEV LidarScene lidar_scene(const ffmp_cfg_t& cfg, double x, double y, double ox, double oy, double r,
+                                bool has) {
+  const double rx = ox - x, ry = oy - y;
+  const double rr = rx * rx + ry * ry;
+  const bool in = has && (rr <= r * r);
+  const double reach = cfg.lidar_max + kLidarCullMargin;
+  const bool act = has && (in || !(sqrt(rr) - r > reach));
+  LidarScene sc;
+  sc.mask = __ballot(act);
+  sc.inside = __any(in);
+  const double W = cfg.world_half;
+  sc.wxp = (W - x) <= reach;
+  sc.wxn = (x + W) <= reach;
+  sc.wyp = (W - y) <= reach;
+  sc.wyn = (y + W) <= reach;
+  return sc;
+}
+
+// One lidar beam (float64): nearest of the scene's discs and walls.  Returns +inf for no
+// return within lidar_max, -inf if the origin is inside a disc.
+FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x, double y, double c, double s,
+                           double bc, double bs, const double* ox, const double* oy, const double* orad) {
+  const double inf = __builtin_inf();
+  if (sc.inside) return -inf;
   const double dirx = c * bc - s * bs;
   const double diry = s * bc + c * bs;
-  const double inf = __builtin_inf();
   double best = inf;
-  bool inside = false;
-  for (int k = 0; k < K; ++k) {
+  for (uint64_t m = sc.mask; m; m &= m - 1) {
+    const int k = __builtin_ctzll(m);
     const double rx = ox[k] - x, ry = oy[k] - y;
     const double rr = rx * rx + ry * ry;
     const double r2 = orad[k] * orad[k];
-    inside |= rr <= r2;
     const double tp = rx * dirx + ry * diry;
     if (tp > 0.0) {
       const double perp = rr - tp * tp;
@@ -235,11 +268,11 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, double x, double y, double c, 
     }
   }
   const double W = cfg.world_half;
-  if (dirx > 0.0) { const double h = (W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; }
-  else if (dirx < 0.0) { const double h = (-W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; }
-  if (diry > 0.0) { const double h = (W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; }
-  else if (diry < 0.0) { const double h = (-W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; }
-  return inside ? -inf : best;
+  if (dirx > 0.0) { if (sc.wxp) { const double h = (W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; } }
+  else if (dirx < 0.0) { if (sc.wxn) { const double h = (-W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; } }
+  if (diry > 0.0) { if (sc.wyp) { const double h = (W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; } }
+  else if (diry < 0.0) { if (sc.wyn) { const double h = (-W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; } }
+  return best;
 }
 
 // FFMP.is_collision2 on one float32 beam (ffmp.py:110-115): `if r:` skips 0,

@@ -65,24 +65,26 @@ int check_cfg(const ffmp_cfg_t* c) {
   return FFMP_OK;
 }
 
-// Raster launch shape.  Defaults are the measured best on MI355X
-// (profiles/r01_raster_tuning.txt): 4096 cells per block; plain stores for
-// planes of more than 16K cells (C3/C5: +1-2.5 %), nontemporal below (C2:
-// +1-3 %).  FFMP_RASTER_CPB (multiple of 1024) and FFMP_RASTER_NT (0/1)
-// override them for tuning sweeps only.
-struct RasterTuning {
-  int cells_per_block = 4096;
-  int nontemporal = -1;  // -1: by plane size
+// Launch-shape tuning.  Defaults are the measured best on MI355X (profiles/r01_*);
+// ffmp_set_tuning() (or the FFMP_RASTER_CPB / FFMP_RASTER_NT / FFMP_RASTER_XCD /
+// FFMP_ENV_WAVES environment variables, read once) overrides them for tuning sweeps.
+struct Tuning {
+  int cells_per_block = 4096;  // raster cells per block (multiple of 1024)
+  int nontemporal = -1;        // raster store flavour: -1 by plane size, 0 plain, 1 nontemporal
+  int xcd_remap = 0;           // 1: each XCD walks its own contiguous range of (env, tile) blocks
+  int env_waves = 1;           // envs (waves) per env_kernel block: 1 or 4
 };
 
-const RasterTuning& raster_tuning() {
-  static const RasterTuning t = [] {
-    RasterTuning r;
+Tuning& tuning() {
+  static Tuning t = [] {
+    Tuning r;
     if (const char* v = getenv("FFMP_RASTER_CPB")) {
       const int c = atoi(v);
       if (c >= 1024 && c % 1024 == 0) r.cells_per_block = c;
     }
     if (const char* v = getenv("FFMP_RASTER_NT")) r.nontemporal = atoi(v) != 0 ? 1 : 0;
+    if (const char* v = getenv("FFMP_RASTER_XCD")) r.xcd_remap = atoi(v) != 0 ? 1 : 0;
+    if (const char* v = getenv("FFMP_ENV_WAVES")) r.env_waves = atoi(v) == 4 ? 4 : 1;
     return r;
   }();
   return t;
@@ -96,18 +98,36 @@ __host__ __device__ inline int64_t rec_stride(int K) { return FFMP_REC_HDR + 8 *
 }  // namespace
 
 // ============================================================================
-// env_kernel: one wave (64 lanes) = one env.
+// env_kernel: one wave (64 lanes) = one env; kEnvWaves envs per block.  Each wave only
+// touches its own LDS slice, so waves synchronise with wave_sync() (no block barrier: waves
+// of one block take different reset branches).
 // ============================================================================
-template <int MODE>
-__global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+
+// Order LDS stores before other lanes' LDS loads within ONE wave (LDS ops of a wave complete
+// in order; the fences stop the compiler from moving them across).
+FFMP_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int MODE, int kEnvWaves>
+__global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                  const int64_t* __restrict__ action,
                                                  const uint8_t* __restrict__ mask, int32_t initial,
                                                  ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
-  __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST];
-  __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
+  __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
+      s_ora[kEnvWaves][FFMP_MAX_OBST];
+  __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
 
-  const int64_t e = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int wv = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * kEnvWaves + wv;
+  const int lane = threadIdx.x & 63;
+  double* s_ox = s_oxa[wv];
+  double* s_oy = s_oya[wv];
+  double* s_or = s_ora[wv];
+  float4* s_ecur = s_ecura[wv];
+  float4* s_eprev = s_epreva[wv];
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
 
@@ -169,7 +189,7 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
   if (has_obst) { s_ox[lane] = my.x; s_oy[lane] = my.y; s_or[lane] = my.r; }
   double c1 = cos(yaw1), s1 = sin(yaw1);
   if (has_obst) s_ecur[lane] = ego_obst(my, x1, y1, c1, s1);
-  __syncthreads();
+  wave_sync();
 
   FrameHdr hcur = make_hdr(x1, y1, c1, s1);
   FrameHdr hprev = (MODE == kEnvMode_Step) ? make_hdr(x0, y0, c0, s0) : hcur;
@@ -186,9 +206,10 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
     }
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
+    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst);
     for (int l = lane; l < L; l += 64) {
-      const double r = lidar_beam(cfg, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_or, K);
+      const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
+                                  s_ox, s_oy, s_or);
       const float rf = (float)r;
       ob.lidar[e * L + l] = rf;
       c_lidar |= beam_collides(rf, cfg.robot_r);
@@ -216,7 +237,7 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
     episode = (MODE == kEnvMode_Reset && initial) ? 0 : episode + 1;
     const Episode ep = sample_episode(cfg, genv, episode);
     x1 = ep.x; y1 = ep.y; yaw1 = ep.yaw; gx = ep.gx; gy = ep.gy;
-    __syncthreads();  // all lanes done reading the terminal-state LDS arrays
+    wave_sync();  // all lanes done reading the terminal-state LDS arrays
     if (has_obst) my = sample_obstacle(cfg, genv, episode, lane, ep);
     c1 = cos(yaw1); s1 = sin(yaw1);
     if (has_obst) {
@@ -225,7 +246,7 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
       s_ecur[lane] = eo;
       s_eprev[lane] = eo;  // temporal stack duplicated on the first step (train.py:475-478)
     }
-    __syncthreads();
+    wave_sync();
     hcur = make_hdr(x1, y1, c1, s1);
     hprev = hcur;
     t = 0;
@@ -238,9 +259,10 @@ __global__ __launch_bounds__(64) void env_kernel(ffmp_cfg_t cfg, int64_t n, int6
       ob.state_g[e * 2 + 0] = (float)dist;
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
+    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst);
     for (int l = lane; l < L; l += 64) {
-      const double r = lidar_beam(cfg, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_or, K);
+      const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
+                                  s_ox, s_oy, s_or);
       ob.lidar[e * L + l] = (float)r;
     }
   }
@@ -341,7 +363,7 @@ FFMP_DEV int small_div(int r, float invG) { return (int)(((float)r + 0.5f) * inv
 
 }  // namespace
 
-template <bool NT>
+template <bool NT, bool XCD>
 __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
@@ -351,8 +373,16 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
   __shared__ float s_hdr[FFMP_REC_HDR];
 
-  const int64_t e = blockIdx.x / bpe;
-  const int tile = (int)(blockIdx.x - e * bpe);
+  // XCD-aware remap: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one), so
+  // logical block (b % 8) * per + b / 8 gives every XCD a contiguous range of (env, tile)
+  // work: 8x less concurrently written footprint per XCD.  A placement-only change.
+  int64_t lb = blockIdx.x;
+  if (XCD) {
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (lb < per * 8) lb = (lb % 8) * per + lb / 8;
+  }
+  const int64_t e = lb / bpe;
+  const int tile = (int)(lb - e * bpe);
   if (e >= n) return;
   if (mask && !mask[e]) return;
 
@@ -540,6 +570,34 @@ int scan_impl(int64_t n, int32_t L, const T* ranges, double thr, uint8_t* collid
 extern "C" {
 
 int ffmp_abi_version(void) { return FFMP_ABI_VERSION; }
+
+int32_t ffmp_set_tuning(int32_t key, int32_t value) {
+  Tuning& t = tuning();
+  int32_t prev;
+  switch (key) {
+    case FFMP_TUNE_RASTER_CPB:
+      if (value != 0 && (value < 1024 || value % 1024 != 0)) return fail(FFMP_E_ARG, "cells per block must be a multiple of 1024");
+      prev = t.cells_per_block;
+      t.cells_per_block = value ? value : 4096;
+      return prev;
+    case FFMP_TUNE_RASTER_NT:
+      if (value < 0 || value > 2) return fail(FFMP_E_ARG, "store flavour must be 0 (auto), 1 (plain) or 2 (nt)");
+      prev = t.nontemporal + 1;
+      t.nontemporal = value - 1;
+      return prev;
+    case FFMP_TUNE_RASTER_XCD:
+      prev = t.xcd_remap;
+      t.xcd_remap = value != 0;
+      return prev;
+    case FFMP_TUNE_ENV_WAVES:
+      if (value != 1 && value != 4) return fail(FFMP_E_ARG, "env waves must be 1 or 4");
+      prev = t.env_waves;
+      t.env_waves = value;
+      return prev;
+    default:
+      return fail(FFMP_E_ARG, "unknown tuning key %d", key);
+  }
+}
 const char* ffmp_last_error(void) { return g_err; }
 
 int64_t ffmp_layout(int32_t which) {
@@ -602,12 +660,23 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
   if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
   ffmp_out_t o = out ? *out : ffmp_out_t{};
   hipStream_t s = (hipStream_t)stream;
-  if (mode == kEnvMode_Step)
-    hipLaunchKernelGGL(env_kernel<kEnvMode_Step>, dim3((unsigned)n), dim3(64), 0, s, *cfg, n, env_offset,
-                       action, mask, initial, *state, *obs, o);
-  else
-    hipLaunchKernelGGL(env_kernel<kEnvMode_Reset>, dim3((unsigned)n), dim3(64), 0, s, *cfg, n, env_offset,
-                       action, mask, initial, *state, *obs, o);
+  const int waves = tuning().env_waves;
+  const unsigned grid1 = (unsigned)n, grid4 = (unsigned)((n + 3) / 4);
+  if (mode == kEnvMode_Step) {
+    if (waves == 4)
+      hipLaunchKernelGGL((env_kernel<kEnvMode_Step, 4>), dim3(grid4), dim3(256), 0, s, *cfg, n, env_offset, action,
+                         mask, initial, *state, *obs, o);
+    else
+      hipLaunchKernelGGL((env_kernel<kEnvMode_Step, 1>), dim3(grid1), dim3(64), 0, s, *cfg, n, env_offset, action,
+                         mask, initial, *state, *obs, o);
+  } else {
+    if (waves == 4)
+      hipLaunchKernelGGL((env_kernel<kEnvMode_Reset, 4>), dim3(grid4), dim3(256), 0, s, *cfg, n, env_offset, action,
+                         mask, initial, *state, *obs, o);
+    else
+      hipLaunchKernelGGL((env_kernel<kEnvMode_Reset, 1>), dim3(grid1), dim3(64), 0, s, *cfg, n, env_offset, action,
+                         mask, initial, *state, *obs, o);
+  }
   return check_launch(mode == kEnvMode_Step ? "ffmp_step_state" : "ffmp_reset");
 }
 
@@ -621,28 +690,47 @@ int ffmp_step_state(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
   return launch_env(kEnvMode_Step, cfg, n, env_offset, action, nullptr, 0, state, obs, out, stream);
 }
 
-int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uint8_t* mask,
-                ffmp_obs_t* obs, void* stream) {
+int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uint8_t* mask,
+                   ffmp_obs_t* obs, int32_t cells_per_block, int32_t flags, void* stream) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
   if (n < 0) return fail(FFMP_E_ARG, "negative n");
   if (!record || !obs || !obs->state_m) return fail(FFMP_E_ARG, "record/obs/state_m is NULL");
+  if (cells_per_block != 0 && (cells_per_block < 1024 || cells_per_block % 1024 != 0))
+    return fail(FFMP_E_ARG, "cells_per_block must be 0 or a multiple of 1024, got %d", cells_per_block);
+  if ((flags & FFMP_RASTER_NT) && (flags & FFMP_RASTER_PLAIN)) return fail(FFMP_E_ARG, "NT and PLAIN both set");
   if (n == 0) return FFMP_OK;
   const int G2 = cfg->grid * cfg->grid;
-  const RasterTuning& tu = raster_tuning();
-  const int cpb_max = tu.cells_per_block;
+  const int cpb_max = cells_per_block ? cells_per_block : 4096;
   const int cpb = G2 < cpb_max ? ((G2 + 1023) / 1024) * 1024 : cpb_max;
   const int bpe = (G2 + cpb - 1) / cpb;
   const int64_t blocks = n * bpe;
   if (blocks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many raster blocks: %lld", (long long)blocks);
-  const bool nt = tu.nontemporal < 0 ? (G2 <= 16384) : (tu.nontemporal != 0);
-  if (nt)
-    hipLaunchKernelGGL(raster_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
-                       bpe, cpb, record, mask, obs->state_m, obs->potential);
+  const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
+  const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
+  const dim3 grid((unsigned)blocks), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (nt && xcd)
+    hipLaunchKernelGGL((raster_kernel<true, true>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, obs->state_m,
+                       obs->potential);
+  else if (nt)
+    hipLaunchKernelGGL((raster_kernel<true, false>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, obs->state_m,
+                       obs->potential);
+  else if (xcd)
+    hipLaunchKernelGGL((raster_kernel<false, true>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask,
+                       obs->state_m, obs->potential);
   else
-    hipLaunchKernelGGL(raster_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *cfg, n,
-                       bpe, cpb, record, mask, obs->state_m, obs->potential);
+    hipLaunchKernelGGL((raster_kernel<false, false>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask,
+                       obs->state_m, obs->potential);
   return check_launch("ffmp_raster");
+}
+
+int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uint8_t* mask, ffmp_obs_t* obs,
+                void* stream) {
+  const Tuning& tu = tuning();
+  const int32_t flags = (tu.nontemporal == 1 ? FFMP_RASTER_NT : tu.nontemporal == 0 ? FFMP_RASTER_PLAIN : 0) |
+                        (tu.xcd_remap ? FFMP_RASTER_XCD : 0);
+  return ffmp_raster_ex(cfg, n, record, mask, obs, tu.cells_per_block, flags, stream);
 }
 
 int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,

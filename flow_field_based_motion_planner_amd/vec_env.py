@@ -50,7 +50,7 @@ class FFMPVec:
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
-                 placement_check: bool = True):
+                 autotune: bool = True, pipeline: Optional[int] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -70,11 +70,17 @@ class FFMPVec:
         self.env_offset = int(env_offset)
         self.with_potential = bool(potential)
         self.arena = bool(arena)
-        self.placement = {"tries": 0, "gbs": None, "all_gbs": []}
+        self.placement = None
+        self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
         self._alloc()
+        G2 = self.cfg.grid * self.cfg.grid
+        if pipeline is None:
+            pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt)
+        self.pipeline_slices = max(1, min(int(pipeline), self.num_envs))
         self._build_structs()
-        if self.arena and placement_check and self._arena_buf.numel() >= self.PLACEMENT_MIN_BYTES:
-            self._place_arena()
+        plane_bytes = self._nbytes((self.num_envs, 3 if potential else 2, G2), torch.float32)
+        if autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
+            self._autotune_raster()
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
@@ -108,91 +114,86 @@ class FFMPVec:
 
     def _alloc(self):
         """All per-shard buffers, zero-initialised.  With arena=True (default) they are views
-        into ONE device allocation carved at 2 MiB boundaries.  Measured on MI355X
-        (profiles/r01_placement.txt): the raster's three concurrent store streams ran at
-        5.8 or 6.9 TB/s depending on how separately allocated planes happened to be placed
-        physically, and at the fast end every time when all planes lived in one allocation."""
+        into ONE device allocation carved at 2 MiB boundaries, planes first."""
         dev = self.device
         specs = self._buffer_specs()
         self.potential = None
         self.lidar = None
         if self.arena:
-            offs, off = [], 0
+            self._arena_offs, off = [], 0
             for _, shape, dtype in specs:
                 off = -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN
-                offs.append(off)
-                n = 1
-                for d in shape:
-                    n *= d
-                off += n * torch.empty((), dtype=dtype).element_size()
-            self._arena_buf = torch.zeros(max(off, 1), dtype=torch.uint8, device=dev)
-            for (name, shape, dtype), o in zip(specs, offs):
-                n = 1
-                for d in shape:
-                    n *= d
-                nb = n * torch.empty((), dtype=dtype).element_size()
-                setattr(self, name, self._arena_buf[o:o + nb].view(dtype).view(shape))
+                self._arena_offs.append(off)
+                off += self._nbytes(shape, dtype)
+            self._arena_used = -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN
+            self._arena_buf = torch.zeros(max(self._arena_used, 1), dtype=torch.uint8, device=dev)
+            self._carve(0)
         else:
             self._arena_buf = None
+            self._arena_used = 0
             for name, shape, dtype in specs:
                 setattr(self, name, torch.zeros(shape, dtype=dtype, device=dev))
         L = self.cfg.n_beams
         self.beam_cs = torch.as_tensor(beam_table(L), dtype=torch.float64).to(dev) if L > 0 else None
 
-    # Placement check (see profiles/r01_placement.txt): the raster's store bandwidth is a
-    # property of the physical memory behind an allocation (measured 5.7-5.8 vs 6.8-7.0 TB/s
-    # for identical virtual layouts, persistent for the life of the allocation).  Time the
-    # raster kernel on the fresh arena; below PLACEMENT_GOOD_GBS, allocate another arena while
-    # still holding the first (so the allocator must hand out different memory) and keep the
-    # fastest of at most PLACEMENT_TRIES.
-    PLACEMENT_MIN_BYTES = 1 << 30
-    PLACEMENT_GOOD_GBS = 6400.0
-    PLACEMENT_TRIES = 4
-    PLACEMENT_SPACER = 3 << 30  # held between candidates so each comes from different memory
+    @staticmethod
+    def _nbytes(shape, dtype) -> int:
+        n = 1
+        for d in shape:
+            n *= d
+        return n * torch.empty((), dtype=dtype).element_size()
 
-    def _raster_gbs(self) -> float:
-        """Raster store bandwidth on the current buffers, measured on a real reset state
-        (a zeroed record would stack every disc on the robot cell: not representative)."""
+    def _carve(self, base: int) -> None:
+        """Point every buffer into the arena, starting `base` bytes in."""
+        self._arena_base = base
+        for (name, shape, dtype), o in zip(self._buffer_specs(), self._arena_offs):
+            nb = self._nbytes(shape, dtype)
+            setattr(self, name, self._arena_buf[base + o:base + o + nb].view(dtype).view(shape))
+
+    # Raster launch-shape autotune (profiles/r01_placement.txt, r01_raster_shapes.txt).  The
+    # raster's three concurrent 16-B store streams run anywhere from 5.7 to 7.3 TB/s depending
+    # on where the planes land in HBM (fixed per allocation, identical virtual layouts) and on
+    # the launch shape, and the best shape differs between allocations (e.g. 4096-cell blocks
+    # 7.1-7.3 TB/s on some allocations and 5.7 on others, where 2048-cell blocks give 6.8).
+    # So the shape is chosen per instance: the raster is timed on this instance's own buffers,
+    # after a real reset, for each candidate, and the fastest is kept.  Results are identical
+    # for every shape.
+    AUTOTUNE_MIN_BYTES = 256 << 20
+    RASTER_SHAPES = (
+        (4096, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN | _abi.RASTER_XCD),
+        (4096, _abi.RASTER_PLAIN | _abi.RASTER_XCD), (2048, _abi.RASTER_NT), (4096, _abi.RASTER_NT),
+    )
+
+    def _raster_gbs_steady(self, steps: int = 3) -> float:
+        """Raster GB/s in the real regime: full steps (env kernel, then raster), raster
+        launches timed with HIP events.  (Back-to-back rasters alone can read up to 15 %
+        higher for some shapes than they sustain inside the step loop.)"""
         from .config import bytes_per_env_step
-        self.reset()
-        with torch.cuda.device(self.device):
-            self.raster()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            ev[0].record()
-            for _ in range(2):
-                self.raster()
-            ev[1].record()
-            torch.cuda.synchronize(self.device)
-        ms = ev[0].elapsed_time(ev[1]) / 2
+        a = torch.full((self.num_envs,), 10, dtype=torch.int64, device=self.device)
+        self.step(a)
+        t = []
+        for _ in range(steps):
+            self.step(a, timing=t)
+        torch.cuda.synchronize(self.device)
+        ms = sum(x.elapsed_time(y) for x, y, _ in t) / len(t)
         b = bytes_per_env_step(self.cfg, potential=self.with_potential)["raster"] * self.num_envs
         return b / (ms * 1e-3) / 1e9
 
-    def _place_arena(self):
-        kept = []  # (gbs, arena tensor, buffers)
-        spacers = []
-        for k in range(self.PLACEMENT_TRIES):
-            if k:
-                spacers.append(torch.empty(self.PLACEMENT_SPACER * k, dtype=torch.uint8, device=self.device))
-                self._alloc()
-                self._build_structs()
-            gbs = self._raster_gbs()
-            self.placement["all_gbs"].append(round(gbs, 1))
-            kept.append((gbs, self._arena_buf, {n: getattr(self, n) for n, _, _ in self._buffer_specs()}))
-            if gbs >= self.PLACEMENT_GOOD_GBS:
-                break
-            free, _ = torch.cuda.mem_get_info(self.device)
-            if free < 1.25 * self._arena_buf.numel() + self.PLACEMENT_SPACER * (k + 1):
-                break  # no room for another candidate arena
-        best = max(range(len(kept)), key=lambda i: kept[i][0])
-        gbs, buf, views = kept[best]
-        self._arena_buf = buf
-        for n, v in views.items():
-            setattr(self, n, v)
-        self._build_structs()
-        self.placement.update(tries=len(kept), gbs=round(gbs, 1))
-        del kept, spacers
-        torch.cuda.empty_cache()
-        self._arena_buf.zero_()
+    def _autotune_raster(self) -> None:
+        self.reset()  # a real state (a zeroed record would stack every disc on the robot cell)
+        results = []
+        plane_bytes = self.state_m.numel() * 4 * (1.5 if self.with_potential else 1.0)
+        steps = 3 if plane_bytes >= (8 << 30) else 12  # >= ~10 ms of timed raster per shape
+        for shape in self.RASTER_SHAPES:
+            self.raster_shape = shape
+            results.append((self._raster_gbs_steady(steps), shape))
+        gbs, shape = max(results)
+        self.raster_shape = shape
+        self.placement = {"shape": {"cells_per_block": shape[0], "flags": shape[1]}, "gbs": round(gbs, 1),
+                          "candidates": [[c, f, round(g, 1)] for g, (c, f) in results]}
+        if self._arena_buf is not None:
+            self._arena_buf.zero_()
+        self._needs_reset = True
 
     def _build_structs(self):
         self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
@@ -204,6 +205,36 @@ class FFMPVec:
                                 _ptr(self.lidar))
         self._out_c = _abi.OutT(self.reward.data_ptr(), self.done.data_ptr(), self.is_goal.data_ptr(),
                                 self.collision.data_ptr(), self.truncated.data_ptr())
+        self._build_slices()
+
+    # Optional pipelined step (pipeline=S > 1): the env kernel of slice s+1 runs on a
+    # high-priority side stream while the raster of slice s runs on the caller's stream.
+    # Results are identical; on MI355X it did not pay (the raster fills every CU, the slices
+    # add kernel tails), so the default is the serial step.
+
+    def _build_slices(self):
+        N, S = self.num_envs, self.pipeline_slices
+        bounds = [N * k // S for k in range(S + 1)]
+
+        def off(t, e0):
+            return None if t is None else t.data_ptr() + e0 * t.stride(0) * t.element_size()
+
+        self._slices = []
+        for k in range(S):
+            a, n = bounds[k], bounds[k + 1] - bounds[k]
+            st = _abi.StateT(off(self.pose, a), off(self.goal, a), off(self.d0, a), off(self.obst, a),
+                             off(self.obst_r, a), off(self.t, a), off(self.episode, a), off(self.record, a),
+                             self.err.data_ptr())
+            ob = _abi.ObsT(off(self.state_m, a), off(self.state_g, a), off(self.state_v, a), off(self.state_t, a),
+                           off(self.potential, a), off(self.grad, a), off(self.lidar, a))
+            out = _abi.OutT(off(self.reward, a), off(self.done, a), off(self.is_goal, a), off(self.collision, a),
+                            off(self.truncated, a))
+            self._slices.append((a, n, st, ob, out, off(self.record, a)))
+        if S > 1 and getattr(self, "_side", None) is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self._side = torch.cuda.Stream(self.device, priority=hi)  # env kernels first
+            self._ev_go = torch.cuda.Event()
+            self._ev_slice = [torch.cuda.Event() for _ in range(S)]
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -238,8 +269,8 @@ class FFMPVec:
             s = self._stream()
             _abi.check(self.lib.ffmp_reset(C.byref(self._cfg_c), self.num_envs, self.env_offset, _ptr(m), initial,
                                            C.byref(self._state_c), C.byref(self._obs_c), s), "ffmp_reset")
-            _abi.check(self.lib.ffmp_raster(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
-                                            C.byref(self._obs_c), s), "ffmp_raster")
+            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
+                                               C.byref(self._obs_c), *self.raster_shape, s), "ffmp_raster")
             self._mask_keepalive = m
         self._needs_reset = False
         return self._obs_out(copy)
@@ -264,16 +295,54 @@ class FFMPVec:
     def raster(self, mask: Optional[torch.Tensor] = None) -> None:
         """Kernel 2 of a step: state_m frames and potential plane (the HBM-bound hot kernel)."""
         m = None if mask is None else mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
-        _abi.check(self.lib.ffmp_raster(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
-                                        C.byref(self._obs_c), self._stream()), "ffmp_raster")
+        _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
+                                           C.byref(self._obs_c), *self.raster_shape, self._stream()), "ffmp_raster")
 
-    def step(self, actions, copy: bool = False) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor, dict]:
-        """Advance every env one step. Returns (obs, reward f32[N], done bool[N], info)."""
+    def _step_pipelined(self, actions, timing) -> None:
+        a = self._actions(actions)
+        self._act_keepalive = a
+        main = torch.cuda.current_stream(self.device)
+        side = self._side
+        self._ev_go.record(main)
+        side.wait_event(self._ev_go)
+        sp = C.c_void_p(side.cuda_stream)
+        for k, (a0, n, st, ob, out, rec) in enumerate(self._slices):
+            _abi.check(self.lib.ffmp_step_state(C.byref(self._cfg_c), n, self.env_offset + a0,
+                                                a.data_ptr() + a0 * 8, C.byref(st), C.byref(ob), C.byref(out), sp),
+                       "ffmp_step_state")
+            self._ev_slice[k].record(side)
+        mp = C.c_void_p(main.cuda_stream)
+        for k, (a0, n, st, ob, out, rec) in enumerate(self._slices):
+            main.wait_event(self._ev_slice[k])
+            if timing is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(main)
+            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), n, rec, None, C.byref(ob), *self.raster_shape, mp),
+                       "ffmp_raster")
+            if timing is not None:
+                e1.record(main)
+                timing.append((e0, e1, n))
+
+    def step(self, actions, copy: bool = False, timing: Optional[list] = None
+             ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor, dict]:
+        """Advance every env one step. Returns (obs, reward f32[N], done bool[N], info).
+
+        `timing`: optional list; (start, end, n_envs) HIP-event pairs around each raster launch
+        (on the caller's stream) are appended to it."""
         if self._needs_reset:
             raise RuntimeError("call reset() before step()")
         with torch.cuda.device(self.device):
-            self.step_state(actions)
-            self.raster()
+            if self.pipeline_slices > 1:
+                self._step_pipelined(actions, timing)
+            else:
+                self.step_state(actions)
+                if timing is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                self.raster()
+                if timing is not None:
+                    e1.record()
+                    timing.append((e0, e1, self.num_envs))
         info = {"is_goal": self.is_goal, "collision": self.collision, "truncated": self.truncated,
                 "step": self.t, "episode": self.episode}
         if copy:

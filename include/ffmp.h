@@ -136,6 +136,14 @@ const char* ffmp_last_error(void);
  * 7 offsetof(ffmp_cfg_t, beam_cs); -1 otherwise. */
 int64_t ffmp_layout(int32_t which);
 
+/* Launch-shape tuning (process-wide; not thread-safe against concurrent launches).
+ * Returns the previous value (>= 0) or FFMP_E_ARG.  Never changes results. */
+#define FFMP_TUNE_RASTER_CPB 1  /* raster cells per block: multiple of 1024; 0 = default   */
+#define FFMP_TUNE_RASTER_NT 2   /* raster stores: 0 by plane size, 1 plain, 2 nontemporal  */
+#define FFMP_TUNE_RASTER_XCD 3  /* 1: XCD-aware block remap                                */
+#define FFMP_TUNE_ENV_WAVES 4   /* envs per env_kernel block: 1 or 4                        */
+int32_t ffmp_set_tuning(int32_t key, int32_t value);
+
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G
  * (map_range = G*res).  Writes up to `cap` offsets (cell - G/2); returns the
  * count, or a negative code. */
@@ -161,6 +169,16 @@ int ffmp_step_state(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
  * potential plane from the raster record (mask NULL = all envs). */
 int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                 const uint8_t* mask, ffmp_obs_t* obs, void* stream);
+
+/* ffmp_raster with an explicit launch shape (results are identical for every shape):
+ * cells_per_block 0 (default 4096) or a multiple of 1024; flags FFMP_RASTER_*
+ * (neither NT nor PLAIN: nontemporal stores for planes of <= 16K cells). */
+#define FFMP_RASTER_NT 1     /* nontemporal 16-B stores          */
+#define FFMP_RASTER_PLAIN 2  /* plain 16-B stores                */
+#define FFMP_RASTER_XCD 4    /* XCD-aware block -> (env, tile) remap */
+int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
+                   const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
+                   int32_t flags, void* stream);
 
 /* ffmp_step_state + ffmp_raster. */
 int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,

@@ -183,3 +183,57 @@ def test_exactness_report(capsys):
     rep = exact_report(gpu_snapshot(env), oracle_snapshot(ref))
     print("non-bit-identical elements:", rep)
     assert rep["record"] == 0
+
+
+@pytest.mark.parametrize("slices", [2, 5])
+def test_pipelined_step_equals_serial(slices):
+    """The two-stream pipelined step (env kernel of slice s+1 beside the raster of slice s)
+    produces exactly the serial step's tensors."""
+    cfg = FFMPConfig(grid=64, n_obst=12, n_beams=32, moving=True, obst_rmax=0.5, seed=41)
+    ser = FFMPVec(83, cfg, device="cuda:0", pipeline=1)
+    pip = FFMPVec(83, cfg, device="cuda:0", pipeline=slices)
+    assert pip.pipeline_slices == slices and ser.pipeline_slices == 1
+    ser.reset()
+    pip.reset()
+    gen = torch.Generator(device="cuda:0").manual_seed(5)
+    for _ in range(8):
+        a = torch.randint(0, 28, (83,), device="cuda:0", generator=gen)
+        t1, t2 = [], []
+        ser.step(a, timing=t1)
+        pip.step(a, timing=t2)
+        assert len(t1) == 1 and len(t2) == slices and sum(n for _, _, n in t2) == 83
+    torch.cuda.synchronize()
+    g1, g2 = gpu_snapshot(ser), gpu_snapshot(pip)
+    for k in g1:
+        if g1[k] is not None:
+            assert np.array_equal(g1[k], g2[k]), k
+
+
+def test_raster_shapes_identical():
+    """Every launch shape the autotuner may pick writes bit-identical planes."""
+    from flow_field_based_motion_planner_amd import _abi
+    cfg = FFMPConfig(grid=128, n_obst=24, n_beams=0, moving=True, obst_rmax=0.8, seed=77)
+    env = FFMPVec(37, cfg, device="cuda:0", autotune=False)
+    env.reset()
+    env.step(torch.randint(0, 28, (37,), device="cuda:0"))
+    ref = None
+    for shape in FFMPVec.RASTER_SHAPES + ((1024, 0), (3072, _abi.RASTER_XCD), (8192, 0)):
+        env.state_m.fill_(-1.0)
+        env.potential.fill_(-1.0)
+        env.raster_shape = shape
+        env.raster()
+        got = (env.state_m.clone(), env.potential.clone())
+        if ref is None:
+            ref = got
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), shape
+
+
+def test_autotune_picks_a_candidate():
+    cfg = FFMPConfig(grid=128, n_obst=8, n_beams=0, seed=3)
+    env = FFMPVec(8192, cfg, device="cuda:0")  # 8192 x 3 x 64 KiB planes > AUTOTUNE_MIN_BYTES
+    assert env.placement is not None
+    assert tuple(env.raster_shape) in FFMPVec.RASTER_SHAPES
+    with pytest.raises(RuntimeError):
+        env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))  # autotune leaves it un-reset
+    env.reset()
+    env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))

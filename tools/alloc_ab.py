@@ -17,7 +17,7 @@ N = 32768
 b = bytes_per_env_step(cfg)["raster"] * N
 for t in range(trials):
     for arena in (True, False):
-        env = FFMPVec(N, cfg, device="cuda:0", arena=arena, placement_check=arena)
+        env = FFMPVec(N, cfg, device="cuda:0", arena=arena, autotune=arena)
         env.reset()
         a = torch.randint(0, 28, (N,), device="cuda:0")
         for _ in range(3):
@@ -30,7 +30,7 @@ for t in range(trials):
         ev[1].record()
         torch.cuda.synchronize()
         ms = ev[0].elapsed_time(ev[1]) / 20
-        print(f"trial {t} arena+check={arena}: raster {ms:.3f} ms  {b / ms / 1e6:.0f} GB/s  placement={env.placement}",
+        print(f"trial {t} arena+autotune={arena}: raster {ms:.3f} ms  {b / ms / 1e6:.0f} GB/s  placement={env.placement}",
               flush=True)
         del env, a
         gc.collect()

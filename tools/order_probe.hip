@@ -15,12 +15,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // MODE 2: tile-major: tile = b / N, e = b % N
 // MODE 3: env-major, pass order rotated per block (start pass = e % passes)
 // MODE 4: env-major, tile rotated by 5*e and pass rotated
+// MODE 5: XCD-aware: block b runs logical block (b % 8) * (nb / 8) + b / 8, so each XCD
+//         (blocks b = x mod 8) walks its own contiguous eighth of the envs
 template <int MODE>
 __global__ __launch_bounds__(256) void three_planes(float* __restrict__ sm, float* __restrict__ pot, int G2, int bpe,
                                                     int cpb, long N) {
   long e;
   int tile;
-  if (MODE == 2) {
+  if (MODE == 5) {
+    const long nb = N * (long)bpe;
+    const long b = blockIdx.x;
+    const long per = nb / 8;
+    const long lb = (b % 8) * per + b / 8;
+    e = lb / bpe;
+    tile = (int)(lb - e * bpe);
+  } else if (MODE == 2) {
     tile = (int)(blockIdx.x / N);
     e = blockIdx.x - (long)tile * N;
   } else {
@@ -71,22 +80,22 @@ int main(int argc, char** argv) {
   const int cpb = argc > 4 ? atoi(argv[4]) : 4096;
   const int G2 = G * G, bpe = (G2 + cpb - 1) / cpb;
   const double bytes = N * 3.0 * G2 * 4;
-  printf("G=%d N=%ld cpb=%d  GB/s per mode: env-major | tile-rot(e) | tile-major | pass-rot | tile-rot(5e)+pass-rot\n", G,
-         N, cpb);
+  printf("G=%d N=%ld  GB/s: env-major cpb=%d | xcd-aware cpb=%d | env-major cpb=1024 | xcd-aware cpb=1024 | env-major cpb=16384\n",
+         G, N, cpb, cpb);
   for (int r = 0; r < allocs; ++r) {
     float *sm, *pot, *junk;
     CHECK(hipMalloc(&junk, (size_t)(r * 37 + 1) << 20));
     CHECK(hipMalloc(&sm, N * 2L * G2 * 4));
     CHECK(hipMalloc(&pot, N * (long)G2 * 4));
+    const int bpe1 = (G2 + 1023) / 1024, bpe16 = (G2 + 16383) / 16384;
     float t[5];
     t[0] = run<0>(sm, pot, G2, bpe, cpb, N);
-    t[1] = run<1>(sm, pot, G2, bpe, cpb, N);
-    t[2] = run<2>(sm, pot, G2, bpe, cpb, N);
-    t[3] = run<3>(sm, pot, G2, bpe, cpb, N);
-    t[4] = run<4>(sm, pot, G2, bpe, cpb, N);
-    float t0b = run<0>(sm, pot, G2, bpe, cpb, N);
-    printf("alloc %d: %.0f | %.0f | %.0f | %.0f | %.0f   (env-major again %.0f)\n", r, bytes / t[0] / 1e6,
-           bytes / t[1] / 1e6, bytes / t[2] / 1e6, bytes / t[3] / 1e6, bytes / t[4] / 1e6, bytes / t0b / 1e6);
+    t[1] = run<5>(sm, pot, G2, bpe, cpb, N);
+    t[2] = run<0>(sm, pot, G2, bpe1, 1024, N);
+    t[3] = run<5>(sm, pot, G2, bpe1, 1024, N);
+    t[4] = run<0>(sm, pot, G2, bpe16, 16384, N);
+    printf("alloc %d: %.0f | %.0f | %.0f | %.0f | %.0f\n", r, bytes / t[0] / 1e6, bytes / t[1] / 1e6,
+           bytes / t[2] / 1e6, bytes / t[3] / 1e6, bytes / t[4] / 1e6);
     CHECK(hipFree(pot));
     CHECK(hipFree(sm));
     CHECK(hipFree(junk));

@@ -11,7 +11,7 @@ from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 
 cfg = preset("C3")
 N = 32768
-env = FFMPVec(N, cfg, device="cuda:0", placement_check=False)
+env = FFMPVec(N, cfg, device="cuda:0", autotune=False)
 env.reset()
 b = bytes_per_env_step(cfg)["raster"] * N
 t0 = time.time()

@@ -161,7 +161,8 @@ class FFMPVec:
     AUTOTUNE_MIN_BYTES = 256 << 20
     RASTER_SHAPES = (
         (4096, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN | _abi.RASTER_XCD),
-        (4096, _abi.RASTER_PLAIN | _abi.RASTER_XCD), (2048, _abi.RASTER_NT), (4096, _abi.RASTER_NT),
+        (4096, _abi.RASTER_PLAIN | _abi.RASTER_XCD), (3072, _abi.RASTER_PLAIN | _abi.RASTER_XCD),
+        (2048, _abi.RASTER_NT), (4096, _abi.RASTER_NT), (2048, _abi.RASTER_NT | _abi.RASTER_XCD),
     )
 
     def _raster_gbs_steady(self, steps: int = 3) -> float:

@@ -77,13 +77,20 @@ def main():
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
                 json.dump({"n_envs": n, "raster_hbm_bytes_per_launch": hb, "source": f"{tag}_{cfg}_pmc.json"}, f,
                           indent=1)
-    if stats:
-        with open(stats) as f:
-            for row in csv.DictReader(f):
-                if "raster_kernel" in row["Name"]:
-                    pm["raster_avg_ns_kernel_trace"] = float(row["AverageNs"])
-                    if bj:
-                        pm["raster_avg_ns_bench_events"] = bj["roofline"]["kernel_ms"] * 1e6
+    trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")
+    if trace and bj:
+        # the last (steps x launches_per_step) raster dispatches are exactly the launches bench.py
+        # timed; earlier ones are warm-up and the per-instance launch-shape autotune
+        rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        k = bj["steps"] * bj["roofline"].get("launches_per_step", 1)
+        timed = rows[-k:]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
+        pm["raster_timed_dispatches"] = len(durs)
+        pm["raster_kernel_name"] = timed[-1]["Kernel_Name"]
+        pm["raster_avg_ns_kernel_trace"] = sum(durs) / len(durs)
+        pm["raster_avg_ns_bench_events"] = bj["roofline"]["kernel_ms"] * 1e6
+        pm["trace_vs_events"] = pm["raster_avg_ns_kernel_trace"] / pm["raster_avg_ns_bench_events"]
     with open(os.path.join(OUT, f"{tag}_{cfg}_pmc.json"), "w") as f:
         json.dump(pm, f, indent=1)
     print(json.dumps(pm, indent=1))

@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--envs", type=int, default=0, help="override envs per rank")
     p.add_argument("--no-potential", action="store_true")
+    p.add_argument("--flow", action="store_true", help="also raster the BEV motion-flow planes (not a BASELINE config)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
@@ -107,7 +108,7 @@ def main():
 
     name = args.config
     pr = PRESETS[name]
-    cfg = preset(name, seed=args.seed)
+    cfg = preset(name, seed=args.seed, flow=args.flow)
     strong = pr["gpus"] > 1
     n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
     # a strong-scaling preset (C4/C5) on fewer GPUs than it is quoted on may not fit one
@@ -172,7 +173,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
-                       "potential": not args.no_potential, "parallelism": f"env-shard x{world}",
+                       "potential": not args.no_potential, "flow": bool(args.flow),
+                       "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class FFMPBackendError(RuntimeError):
@@ -27,6 +27,7 @@ class CfgT(C.Structure):
     _fields_ = [
         ("grid", C.c_int32), ("n_obst", C.c_int32), ("n_beams", C.c_int32), ("max_steps", C.c_int32),
         ("moving", C.c_int32), ("autoreset", C.c_int32), ("collide_mode", C.c_int32), ("n_foot", C.c_int32),
+        ("flow", C.c_int32), ("reserved0", C.c_int32),
         ("foot_di", C.c_int32 * MAX_FOOT), ("foot_dj", C.c_int32 * MAX_FOOT),
         ("res", C.c_double), ("dt", C.c_double), ("robot_r", C.c_double), ("goal_thr", C.c_double),
         ("world_half", C.c_double), ("lidar_max", C.c_double), ("goal_min", C.c_double), ("goal_max", C.c_double),
@@ -47,7 +48,8 @@ class StateT(C.Structure):
 
 class ObsT(C.Structure):
     _fields_ = [("state_m", C.c_void_p), ("state_g", C.c_void_p), ("state_v", C.c_void_p),
-                ("state_t", C.c_void_p), ("potential", C.c_void_p), ("grad", C.c_void_p), ("lidar", C.c_void_p)]
+                ("state_t", C.c_void_p), ("potential", C.c_void_p), ("grad", C.c_void_p), ("lidar", C.c_void_p),
+                ("flow", C.c_void_p)]
 
 
 class OutT(C.Structure):
@@ -59,6 +61,7 @@ def make_cfg(cfg: FFMPConfig, beam_cs_ptr: int = 0) -> CfgT:
     c = CfgT()
     c.grid, c.n_obst, c.n_beams, c.max_steps = cfg.grid, cfg.n_obst, cfg.n_beams, cfg.max_steps
     c.moving, c.autoreset, c.collide_mode = int(cfg.moving), int(cfg.autoreset), cfg.mode
+    c.flow = int(bool(cfg.flow))
     fp = cfg.footprint
     c.n_foot = len(fp)
     for k, (di, dj) in enumerate(fp):

@@ -98,6 +98,7 @@ class FFMPConfig:
     rho0: float = 0.5
     rho_min: Optional[float] = None      # default res/2
     cull_margin: float = 0.1
+    flow: bool = False              # also raster the BEV motion-flow planes
     seed: int = 0
 
     # ---- derived -----------------------------------------------------------
@@ -162,7 +163,7 @@ class FFMPConfig:
         }
 
     def record_len(self) -> int:
-        return REC_HDR + 8 * self.n_obst
+        return REC_HDR + 12 * self.n_obst
 
     def replace(self, **kw) -> "FFMPConfig":
         return dataclasses.replace(self, **kw)
@@ -193,15 +194,16 @@ def preset(name: str, **overrides) -> FFMPConfig:
 def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True) -> Dict[str, int]:
     """Algorithmic HBM bytes of one env step.
 
-    raster kernel: writes both float32 frames of state_m (8 G^2) and the float32
-    potential plane (4 G^2); reads the raster record (64 + 32 K).  state kernel:
+    raster kernel: writes both float32 frames of state_m (8 G^2), the float32
+    potential plane (4 G^2) and, with cfg.flow, the two float32 flow planes (8 G^2);
+    reads the raster record (64 + 48 K).  state kernel:
     reads/writes pose, goal, d0, t, episode, obstacles and writes the small obs,
     lidar and the record.
     """
     G2 = cfg.grid * cfg.grid
     K, L = cfg.n_obst, cfg.n_beams
     rec = 4 * cfg.record_len()
-    raster = 8 * G2 + (4 * G2 if potential else 0) + rec
+    raster = 8 * G2 + (4 * G2 if potential else 0) + (8 * G2 if cfg.flow else 0) + rec
     state_rw = 2 * (24 + 16 + 8 + 4 + 4 + 40 * K)  # pose, goal, d0, t, episode, obst(32)+r(8)
     small_obs = 4 * (2 + 2 + 1 + 2) + 4 * L + rec + 8 + 4 + 4  # g, v, t, grad, lidar, record, action, reward, flags
     return {"raster": raster, "state": state_rw + small_obs, "total": raster + state_rw + small_obs}

@@ -134,7 +134,8 @@ FFMP_DEV void move_obstacle(const ffmp_cfg_t& cfg, Obst& o) {
 // ---------------- raster record (per env, float32) ---------------------------
 // hdr[0..3] current frame {px, py, cos yaw, sin yaw}; hdr[4..7] previous frame;
 // hdr[8..9] goal in the current ego frame; then K float4 {ox, oy, r*r, r} of the
-// current frame in ego coordinates, then K float4 of the previous frame.
+// current frame in ego coordinates, K float4 of the previous frame, and K float4
+// {vx, vy, 0, 0}: each disc's velocity rotated into the current ego frame.
 struct FrameHdr {
   float px, py, c, s;
 };
@@ -149,6 +150,13 @@ FFMP_DEV float2 to_ego(double wx, double wy, double x, double y, double c, doubl
   const double ex = c * rx + s * ry;
   const double ey = c * ry - s * rx;
   return make_float2((float)ex, (float)ey);
+}
+
+// World velocity -> current ego frame (float64 rotation, rounded to float32).
+FFMP_DEV float4 ego_vel(const Obst& o, double c, double s) {
+  const double vx = c * o.vx + s * o.vy;
+  const double vy = c * o.vy - s * o.vx;
+  return make_float4((float)vx, (float)vy, 0.0f, 0.0f);
 }
 
 FFMP_DEV float4 ego_obst(const Obst& o, double x, double y, double c, double s) {

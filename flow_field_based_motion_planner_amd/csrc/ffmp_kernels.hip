@@ -93,7 +93,7 @@ Tuning& tuning() {
 constexpr int kEnvMode_Step = 0;
 constexpr int kEnvMode_Reset = 1;
 
-__host__ __device__ inline int64_t rec_stride(int K) { return FFMP_REC_HDR + 8 * (int64_t)K; }
+__host__ __device__ inline int64_t rec_stride(int K) { return FFMP_REC_HDR + 12 * (int64_t)K; }
 
 }  // namespace
 
@@ -295,6 +295,7 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
       float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
       ro[lane] = s_ecur[lane];
       ro[K + lane] = s_eprev[lane];
+      ro[2 * K + lane] = ego_vel(my, c1, s1);
     }
   }
 
@@ -363,14 +364,16 @@ FFMP_DEV int small_div(int r, float invG) { return (int)(((float)r + 0.5f) * inv
 
 }  // namespace
 
-template <bool NT, bool XCD>
+template <bool NT, bool XCD, bool FLOW>
 __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
                                                      const uint8_t* __restrict__ mask,
                                                      float* __restrict__ state_m,
-                                                     float* __restrict__ pot) {
+                                                     float* __restrict__ pot,
+                                                     float* __restrict__ flow) {
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
+  __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
   __shared__ float s_hdr[FFMP_REC_HDR];
 
   // XCD-aware remap: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one), so
@@ -396,6 +399,10 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
     const float4* ro = reinterpret_cast<const float4*>(rec + FFMP_REC_HDR);
     s_cur[tid] = ro[tid];
     s_prev[tid] = ro[K + tid];
+    if (FLOW) {
+      const float4 v = ro[2 * K + tid];
+      s_vel[tid] = make_float2(v.x, v.y);
+    }
   }
   __syncthreads();
 
@@ -419,6 +426,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   float* m0 = state_m + (int64_t)e * 2 * G2;
   float* m1 = m0 + G2;
   float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
+  float* f0 = FLOW ? flow + (int64_t)e * 2 * G2 : nullptr;
 
   const int qbeg = tile * cells_per_block;
   const int qend = min(qbeg + cells_per_block, G2);
@@ -466,17 +474,30 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
 #pragma unroll
       for (int u = 0; u < 4; ++u) if (in_disc(ex, ey[u], o)) occp[u] = 1.0f;
     }
+    float fx[4] = {0.f, 0.f, 0.f, 0.f}, fy[4] = {0.f, 0.f, 0.f, 0.f};
+    bool fset[4] = {false, false, false, false};
     for (uint64_t m = mc; m; m &= m - 1) {
-      const float4 o = s_cur[__builtin_ctzll(m)];
+      const int k = __builtin_ctzll(m);
+      const float4 o = s_cur[k];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (in_disc(ex, ey[u], o)) occc[u] = 1.0f;
+        const bool d = in_disc(ex, ey[u], o);
+        if (d) occc[u] = 1.0f;
+        if (FLOW && d && !fset[u]) {  // lowest disc index covering the cell
+          fx[u] = s_vel[k].x;
+          fy[u] = s_vel[k].y;
+          fset[u] = true;
+        }
         U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
       }
     }
     store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
     store4<NT>(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
     if (pp) store4<NT>(pp + q, U[0], U[1], U[2], U[3]);
+    if (FLOW) {
+      store4<NT>(f0 + q, fx[0], fx[1], fx[2], fx[3]);
+      store4<NT>(f0 + G2 + q, fy[0], fy[1], fy[2], fy[3]);
+    }
   }
 }
 
@@ -708,20 +729,25 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   if (blocks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many raster blocks: %lld", (long long)blocks);
   const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
   const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
+  const bool fl = cfg->flow != 0;
+  if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
   const dim3 grid((unsigned)blocks), block(256);
   hipStream_t s = (hipStream_t)stream;
-  if (nt && xcd)
-    hipLaunchKernelGGL((raster_kernel<true, true>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, obs->state_m,
-                       obs->potential);
-  else if (nt)
-    hipLaunchKernelGGL((raster_kernel<true, false>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, obs->state_m,
-                       obs->potential);
-  else if (xcd)
-    hipLaunchKernelGGL((raster_kernel<false, true>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask,
-                       obs->state_m, obs->potential);
-  else
-    hipLaunchKernelGGL((raster_kernel<false, false>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask,
-                       obs->state_m, obs->potential);
+#define FFMP_RASTER_LAUNCH(NT_, XCD_, FL_)                                                              \
+  hipLaunchKernelGGL((raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, \
+                     obs->state_m, obs->potential, obs->flow)
+  const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
+  switch (sel) {
+    case 0: FFMP_RASTER_LAUNCH(false, false, false); break;
+    case 1: FFMP_RASTER_LAUNCH(false, false, true); break;
+    case 2: FFMP_RASTER_LAUNCH(false, true, false); break;
+    case 3: FFMP_RASTER_LAUNCH(false, true, true); break;
+    case 4: FFMP_RASTER_LAUNCH(true, false, false); break;
+    case 5: FFMP_RASTER_LAUNCH(true, false, true); break;
+    case 6: FFMP_RASTER_LAUNCH(true, true, false); break;
+    default: FFMP_RASTER_LAUNCH(true, true, true); break;
+  }
+#undef FFMP_RASTER_LAUNCH
   return check_launch("ffmp_raster");
 }
 

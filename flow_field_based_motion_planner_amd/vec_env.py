@@ -78,7 +78,8 @@ class FFMPVec:
             pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt)
         self.pipeline_slices = max(1, min(int(pipeline), self.num_envs))
         self._build_structs()
-        plane_bytes = self._nbytes((self.num_envs, 3 if potential else 2, G2), torch.float32)
+        plane_bytes = self._nbytes((self.num_envs, (3 if potential else 2) + (2 if self.cfg.flow else 0), G2),
+                                   torch.float32)
         if autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
             self._autotune_raster()
         self._needs_reset = True
@@ -95,6 +96,7 @@ class FFMPVec:
             # observation planes first: the big, hot, write-streamed buffers
             ("state_m", (N, 2, G, G), f32),
             ("potential", (N, G, G), f32),
+            ("flow", (N, 2, G, G), f32),
             # state
             ("pose", (N, 3), f64), ("goal", (N, 2), f64), ("d0", (N,), f64),
             ("obst", (N, max(K, 1), 4), f64), ("obst_r", (N, max(K, 1)), f64),
@@ -108,6 +110,8 @@ class FFMPVec:
         ]
         if not self.with_potential:
             specs = [sp for sp in specs if sp[0] != "potential"]
+        if not cfg.flow:
+            specs = [sp for sp in specs if sp[0] != "flow"]
         if L == 0:
             specs = [sp for sp in specs if sp[0] != "lidar"]
         return specs
@@ -119,6 +123,7 @@ class FFMPVec:
         specs = self._buffer_specs()
         self.potential = None
         self.lidar = None
+        self.flow = None
         if self.arena:
             self._arena_offs, off = [], 0
             for _, shape, dtype in specs:
@@ -183,7 +188,7 @@ class FFMPVec:
     def _autotune_raster(self) -> None:
         self.reset()  # a real state (a zeroed record would stack every disc on the robot cell)
         results = []
-        plane_bytes = self.state_m.numel() * 4 * (1.5 if self.with_potential else 1.0)
+        plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) + (1.0 if self.flow is not None else 0.0))
         steps = 3 if plane_bytes >= (8 << 30) else 12  # >= ~10 ms of timed raster per shape
         for shape in self.RASTER_SHAPES:
             self.raster_shape = shape
@@ -203,7 +208,7 @@ class FFMPVec:
                                     self.episode.data_ptr(), self.record.data_ptr(), self.err.data_ptr())
         self._obs_c = _abi.ObsT(self.state_m.data_ptr(), self.state_g.data_ptr(), self.state_v.data_ptr(),
                                 self.state_t.data_ptr(), _ptr(self.potential), self.grad.data_ptr(),
-                                _ptr(self.lidar))
+                                _ptr(self.lidar), _ptr(self.flow))
         self._out_c = _abi.OutT(self.reward.data_ptr(), self.done.data_ptr(), self.is_goal.data_ptr(),
                                 self.collision.data_ptr(), self.truncated.data_ptr())
         self._build_slices()
@@ -227,7 +232,7 @@ class FFMPVec:
                              off(self.obst_r, a), off(self.t, a), off(self.episode, a), off(self.record, a),
                              self.err.data_ptr())
             ob = _abi.ObsT(off(self.state_m, a), off(self.state_g, a), off(self.state_v, a), off(self.state_t, a),
-                           off(self.potential, a), off(self.grad, a), off(self.lidar, a))
+                           off(self.potential, a), off(self.grad, a), off(self.lidar, a), off(self.flow, a))
             out = _abi.OutT(off(self.reward, a), off(self.done, a), off(self.is_goal, a), off(self.collision, a),
                             off(self.truncated, a))
             self._slices.append((a, n, st, ob, out, off(self.record, a)))
@@ -249,6 +254,8 @@ class FFMPVec:
             d["potential"] = self.potential
         if self.lidar is not None:
             d["lidar"] = self.lidar
+        if self.flow is not None:
+            d["flow"] = self.flow
         return d
 
     def _obs_out(self, copy: bool):

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 1
+#define FFMP_ABI_VERSION 2
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -66,6 +66,8 @@ typedef struct ffmp_cfg {
   int32_t autoreset;     /* 1: ffmp_step resets done envs in place */
   int32_t collide_mode;  /* FFMP_COLLIDE_* bits */
   int32_t n_foot;        /* number of footprint offsets below */
+  int32_t flow;          /* 1: raster the BEV motion-flow planes (obs.flow) */
+  int32_t reserved0;
   int32_t foot_di[FFMP_MAX_FOOT]; /* footprint cell offsets from (G/2, G/2) */
   int32_t foot_dj[FFMP_MAX_FOOT];
   double res;            /* m per cell (ffmp.py:18, 0.05) */
@@ -102,7 +104,7 @@ typedef struct ffmp_state {
   double* obst_r;   /* (N,K) radius                                  */
   int32_t* t;       /* (N)   steps since episode start               */
   int32_t* episode; /* (N)   episode counter (RNG key part)          */
-  float* record;    /* (N, FFMP_REC_HDR + 8K) raster record */
+  float* record;    /* (N, FFMP_REC_HDR + 12K) raster record */
   uint32_t* err;    /* (1)   sticky error bits (bit0: bad action id) */
 } ffmp_state_t;
 
@@ -116,6 +118,8 @@ typedef struct ffmp_obs {
   float* potential; /* (N,G,G) attractive+repulsive potential, or NULL */
   float* grad;      /* (N,2) central-difference gradient at robot cell */
   float* lidar;     /* (N,L) ranges (+inf = no return, -inf = inside), NULL if L == 0 */
+  float* flow;      /* (N,2,G,G) ego-frame velocity (m/s) of the disc covering each cell of the
+                       newest frame (lowest disc index wins), 0 elsewhere; NULL unless cfg.flow */
 } ffmp_obs_t;
 
 /* Per-step outputs (device pointers, N each). Flags are 0/1 bytes. */

@@ -16,6 +16,7 @@ def gpu_snapshot(env, sl=slice(None)):
           "truncated", "pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record")}
     d["potential"] = env.potential[sl].detach().cpu().numpy() if env.potential is not None else None
     d["lidar"] = env.lidar[sl].detach().cpu().numpy() if env.lidar is not None else None
+    d["flow"] = env.flow[sl].detach().cpu().numpy() if env.flow is not None else None
     K = env.cfg.n_obst
     if K == 0:
         d["obst"] = d["obst"][:, :0]
@@ -29,6 +30,7 @@ def oracle_snapshot(ref):
           "truncated", "pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record")}
     d["potential"] = ref.potential if ref.with_potential else None
     d["lidar"] = ref.lidar if ref.cfg.n_beams else None
+    d["flow"] = ref.flow
     return d
 
 
@@ -44,6 +46,10 @@ def compare(g, o, where=""):
         ne = ~((a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b))
         return int(ne.sum())
 
+    if (g.get("flow") is None) != (o.get("flow") is None):
+        bad.append(f"{where} flow: present on one side only")
+    elif g.get("flow") is not None and not np.array_equal(g["flow"], o["flow"]):
+        bad.append(f"{where} flow: {int((g['flow'] != o['flow']).sum())} elements differ")
     for k in EXACT_FIELDS + ("record",):
         c = diff_count(g[k], o[k])
         if c:

@@ -25,6 +25,8 @@ CASES = {
                                     world_half=3.2, goal_max=2.0, seed=5), 48, 40),
     "C5_512_moving_lidar": (FFMPConfig(grid=512, n_obst=32, n_beams=360, moving=True, seed=6), 2, 4),
     "no_obstacles": (FFMPConfig(grid=32, n_obst=0, n_beams=8, moving=False, max_steps=5, seed=7), 8, 12),
+    "flow_planes": (FFMPConfig(grid=128, n_obst=24, n_beams=64, moving=True, flow=True, obst_rmax=0.7,
+                               obst_vmax=1.2, seed=8), 12, 15),
 }
 
 

@@ -153,3 +153,28 @@ def test_invalid_actions_flagged():
     env.step(np.array([3, 99]))
     assert env.err == 1
     assert np.array_equal(env.pose[1], before[1])  # treated as action 3 (0, 0): no motion
+
+
+def test_flow_planes_semantics():
+    """BEV motion flow: nonzero only on disc-occupied cells of the newest
+    frame, equal to the covering disc's ego-frame velocity (lowest index wins)."""
+    cfg = FFMPConfig(grid=64, n_obst=10, n_beams=0, moving=True, flow=True, obst_rmax=0.6, obst_vmax=1.0, seed=8)
+    env = O.OracleVecEnv(cfg, 6)
+    env.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(4):
+        env.step(rng.integers(0, 28, 6))
+        f = env.flow
+        moving = (f[:, 0] != 0) | (f[:, 1] != 0)
+        assert not moving[env.state_m[:, 1] == 0].any()
+        assert np.all(np.hypot(f[:, 0], f[:, 1]) <= cfg.obst_vmax * (1 + 1e-6))
+    # static discs -> all-zero flow
+    st = O.OracleVecEnv(cfg.replace(moving=False), 3)
+    st.reset()
+    st.step(np.zeros(3, dtype=np.int64))
+    assert not st.flow.any()
+    # speed of every flow vector equals its disc's world speed (rotation preserves length)
+    rec = O.Record.unpack(env.record, cfg.n_obst)
+    sp_world = np.hypot(env.obst[:, :, 2], env.obst[:, :, 3])
+    sp_ego = np.hypot(rec.vel[:, :, 0].astype(np.float64), rec.vel[:, :, 1].astype(np.float64))
+    assert np.allclose(sp_world, sp_ego, atol=1e-6)

@@ -82,6 +82,8 @@ class FFMPVec:
                                    torch.float32)
         if autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
             self._autotune_raster()
+            if self.arena and plane_bytes >= self.REPLACE_MIN_BYTES:
+                self._retry_placement()
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
@@ -184,6 +186,46 @@ class FFMPVec:
         ms = sum(x.elapsed_time(y) for x, y, _ in t) / len(t)
         b = bytes_per_env_step(self.cfg, potential=self.with_potential)["raster"] * self.num_envs
         return b / (ms * 1e-3) / 1e9
+
+    # Placement retries.  Even the best shape runs ~15 % slower on a "slow" placement (e.g.
+    # C3: 6.2-6.3 vs 7.1-7.3 TB/s), and allocating again while the first arena and a spacer
+    # are still held (so the allocator must return different memory) often lands fast.  If the
+    # tuned bandwidth is below PLACEMENT_FAST_GBS, up to PLACEMENT_RETRIES further arenas are
+    # tried (each autotuned) and the fastest kept; bounded by free HBM.
+    REPLACE_MIN_BYTES = 4 << 30
+    PLACEMENT_FAST_GBS = 6800.0
+    PLACEMENT_RETRIES = 3
+    PLACEMENT_SPACER = 1 << 30
+
+    def _retry_placement(self) -> None:
+        names = [n for n, _, _ in self._buffer_specs()]
+        keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names}, self.raster_shape,
+                 self.placement)]
+        spacers = []
+        tries = [round(self.placement["gbs"], 1)]
+        for k in range(self.PLACEMENT_RETRIES):
+            if max(c[0] for c in keep) >= self.PLACEMENT_FAST_GBS:
+                break
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if free < 1.2 * self._arena_buf.numel() + (k + 1) * self.PLACEMENT_SPACER + (1 << 30):
+                break
+            spacers.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
+            self._alloc()
+            self._build_structs()
+            self._autotune_raster()
+            tries.append(round(self.placement["gbs"], 1))
+            keep.append((self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
+                         self.raster_shape, self.placement))
+        best = max(range(len(keep)), key=lambda i: keep[i][0])
+        _, buf, views, shape, placement = keep[best]
+        self._arena_buf = buf
+        for n, v in views.items():
+            setattr(self, n, v)
+        self.raster_shape = shape
+        self.placement = dict(placement, placement_tries=tries, placement_kept=best)
+        self._build_structs()
+        del keep, spacers, views, buf
+        torch.cuda.empty_cache()
 
     def _autotune_raster(self) -> None:
         self.reset()  # a real state (a zeroed record would stack every disc on the robot cell)

@@ -19,6 +19,9 @@ def __getattr__(name):  # lazy: torch / the HIP library load only when used
     if name == "FFMP":
         from .env import FFMP
         return FFMP
+    if name == "EpisodeTracker":
+        from .episodes import EpisodeTracker
+        return EpisodeTracker
     raise AttributeError(name)
 
 

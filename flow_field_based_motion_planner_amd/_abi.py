@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class FFMPBackendError(RuntimeError):
@@ -55,6 +55,14 @@ class ObsT(C.Structure):
 class OutT(C.Structure):
     _fields_ = [("reward", C.c_void_p), ("done", C.c_void_p), ("is_goal", C.c_void_p),
                 ("collide", C.c_void_p), ("truncated", C.c_void_p)]
+
+
+class EpisodeT(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("reach_bits", "reach_len", "reach_rate", "step", "episode",
+                                          "total_step", "is_first", "complete", "totals")]
+
+
+EP_TOTALS = 8
 
 
 def make_cfg(cfg: FFMPConfig, beam_cs_ptr: int = 0) -> CfgT:
@@ -98,6 +106,9 @@ _SIGS = {
     "ffmp_footprint_collision": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I64, _P, _P]),
     "ffmp_scan_collision": (C.c_int, [_I64, _I32, _P, C.c_double, _P, _P, _P]),
     "ffmp_scan_collision_f64": (C.c_int, [_I64, _I32, _P, C.c_double, _P, _P, _P]),
+    "ffmp_episode_init": (C.c_int, [_I64, _P, C.POINTER(EpisodeT), _P]),
+    "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
+                                      _P]),
 }
 
 _LIB: Optional[C.CDLL] = None
@@ -162,6 +173,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
     want = {
         0: C.sizeof(CfgT), 1: C.sizeof(StateT), 2: C.sizeof(ObsT), 3: C.sizeof(OutT),
         4: CfgT.res.offset, 5: CfgT.res_f.offset, 6: CfgT.seed.offset, 7: CfgT.beam_cs.offset,
+        8: C.sizeof(EpisodeT),
     }
     for k, v in want.items():
         got = lib.ffmp_layout(k)

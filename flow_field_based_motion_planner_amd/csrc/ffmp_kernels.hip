@@ -585,6 +585,83 @@ int scan_impl(int64_t n, int32_t L, const T* ranges, double thr, uint8_t* collid
   return check_launch("ffmp_scan_collision");
 }
 
+
+// ============================================================================
+// Episode bookkeeping (src/train.py:501-505, 579-587, 593, 607, 611-682), one thread per env.
+// Counts for totals[] are wave ballots: one atomic per counter per wave.
+// ============================================================================
+__device__ __forceinline__ void wave_count(uint64_t* totals, int k, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long*)&totals[k], (unsigned long long)__popcll(m));
+}
+
+__global__ __launch_bounds__(256) void episode_init_kernel(int64_t n, const uint8_t* __restrict__ mask,
+                                                           ffmp_episode_t ep) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ep.totals && !mask && e < FFMP_EP_TOTALS) ep.totals[e] = 0;
+  if (e >= n || (mask && !mask[e])) return;
+  ep.reach_bits[e] = 0;
+  ep.reach_len[e] = 0;
+  ep.reach_rate[e] = 0.0;
+  ep.step[e] = 0;
+  ep.episode[e] = 0;
+  ep.total_step[e] = 0;
+  ep.is_first[e] = 1;
+  ep.complete[e] = 0;
+}
+
+__global__ __launch_bounds__(256) void episode_update_kernel(int64_t n, ffmp_out_t out, int32_t window,
+                                                             int32_t max_steps, double threshold, int32_t armed,
+                                                             ffmp_episode_t ep) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = e < n;
+  bool goal = false, done = false, trunc = false, col = false, fin = false;
+  if (act) {
+    goal = out.is_goal[e] != 0;
+    col = out.collide[e] != 0;
+    const int32_t step = ep.step[e];
+    // :579-587  reach_times.append(is_goal); keep the last REACH_MEMORY_CAPACITY; np.average
+    const uint64_t keep = window >= 64 ? ~0ull : ((1ull << window) - 1ull);
+    const uint64_t bits = ((ep.reach_bits[e] << 1) | (goal ? 1ull : 0ull)) & keep;
+    const int32_t len = min(ep.reach_len[e] + 1, window);
+    const double rate = (double)__popcll(bits) / (double)len;
+    ep.reach_bits[e] = bits;
+    ep.reach_len[e] = len;
+    ep.reach_rate[e] = rate;
+    // :607  if step == MAX_STEPS: is_done = True
+    const bool own_trunc = max_steps > 0 && step == max_steps;
+    done = (out.done[e] != 0) || own_trunc;
+    trunc = done && ((out.truncated[e] != 0) || (own_trunc && !out.done[e]));
+    if (done) {  // :611-663
+      ep.episode[e] += 1;
+      ep.step[e] = 0;
+      ep.is_first[e] = 1;
+      fin = armed && rate > threshold;  // :644
+      if (fin) ep.complete[e] = 1;
+    } else {  // :593, :681-682
+      ep.step[e] = step + 1;
+      ep.total_step[e] += 1;
+      ep.is_first[e] = 0;
+    }
+  }
+  if (ep.totals) {
+    wave_count(ep.totals, 0, act);
+    wave_count(ep.totals, 1, done);
+    wave_count(ep.totals, 2, goal);
+    wave_count(ep.totals, 3, col);
+    wave_count(ep.totals, 4, trunc);
+    wave_count(ep.totals, 5, fin);
+    wave_count(ep.totals, 6, act && !done);
+  }
+}
+
+static int check_episode(const ffmp_episode_t* ep) {
+  if (!ep || !ep->reach_bits || !ep->reach_len || !ep->reach_rate || !ep->step || !ep->episode ||
+      !ep->total_step || !ep->is_first || !ep->complete)
+    return fail(FFMP_E_ARG, "episode struct or one of its arrays is NULL");
+  return FFMP_OK;
+}
+
 // ============================================================================
 // C ABI
 // ============================================================================
@@ -631,6 +708,7 @@ int64_t ffmp_layout(int32_t which) {
     case 5: return (int64_t)offsetof(ffmp_cfg_t, res_f);
     case 6: return (int64_t)offsetof(ffmp_cfg_t, seed);
     case 7: return (int64_t)offsetof(ffmp_cfg_t, beam_cs);
+    case 8: return (int64_t)sizeof(ffmp_episode_t);
     default: return -1;
   }
 }
@@ -804,6 +882,29 @@ int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr, u
 int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr, uint8_t* collide,
                             double* min_r, void* stream) {
   return scan_impl<double>(n, L, ranges, thr, collide, min_r, stream);
+}
+
+int ffmp_episode_init(int64_t n, const uint8_t* mask, ffmp_episode_t* ep, void* stream) {
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (const int rc = check_episode(ep)) return rc;
+  const int64_t m = n > FFMP_EP_TOTALS ? n : FFMP_EP_TOTALS;
+  hipLaunchKernelGGL(episode_init_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                     mask, *ep);
+  return check_launch("ffmp_episode_init");
+}
+
+int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps, double threshold,
+                        int32_t armed, ffmp_episode_t* ep, void* stream) {
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (window < 1 || window > 64) return fail(FFMP_E_ARG, "window must be in [1, 64], got %d", window);
+  if (max_steps < 0) return fail(FFMP_E_ARG, "negative max_steps");
+  if (!out || !out->done || !out->is_goal || !out->collide || !out->truncated)
+    return fail(FFMP_E_ARG, "out or one of its flag arrays is NULL");
+  if (const int rc = check_episode(ep)) return rc;
+  if (n == 0) return FFMP_OK;
+  hipLaunchKernelGGL(episode_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     n, *out, window, max_steps, threshold, armed, *ep);
+  return check_launch("ffmp_episode_update");
 }
 
 }  // extern "C"

@@ -25,6 +25,11 @@
  *   ffmp_scan_collision[_f64] -> FFMP.is_collision2 (ffmp.py:108-117)
  *   ffmp_footprint      -> the robot_grids mask built inside is_collision
  *                          (ffmp.py:87-94), host-side, float64
+ *   ffmp_episode_init / ffmp_episode_update -> the main loop's episode
+ *                          bookkeeping: counters src/train.py:501-505, reach_times /
+ *                          reach_rate :579-587 (REACH_MEMORY_CAPACITY :76), is_first
+ *                          :593,662, truncation :607, the is_done branch :611-682
+ *                          (episode / step / total_step, completion test :644)
  */
 #ifndef FFMP_H
 #define FFMP_H
@@ -35,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 2
+#define FFMP_ABI_VERSION 3
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -137,7 +142,7 @@ const char* ffmp_last_error(void);
 /* Layout check for FFI bindings: which = 0 sizeof(ffmp_cfg_t), 1 sizeof(ffmp_state_t),
  * 2 sizeof(ffmp_obs_t), 3 sizeof(ffmp_out_t), 4 offsetof(ffmp_cfg_t, res),
  * 5 offsetof(ffmp_cfg_t, res_f), 6 offsetof(ffmp_cfg_t, seed),
- * 7 offsetof(ffmp_cfg_t, beam_cs); -1 otherwise. */
+ * 7 offsetof(ffmp_cfg_t, beam_cs), 8 sizeof(ffmp_episode_t); -1 otherwise. */
 int64_t ffmp_layout(int32_t which);
 
 /* Launch-shape tuning (process-wide; not thread-safe against concurrent launches).
@@ -214,6 +219,38 @@ int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr,
                         uint8_t* collide, float* min_r, void* stream);
 int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr,
                             uint8_t* collide, double* min_r, void* stream);
+
+/* Episode bookkeeping of the training loop, batched (one record per env, device memory).
+ * Per env and per ffmp_episode_update, exactly as src/train.py:579-682 does per iteration:
+ *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)
+ *   reach_rate    =  np.average(window)                                    (:587, float64)
+ *   done          =  out.done || (max_steps > 0 && step == max_steps)      (:607)
+ *   done:  episode += 1, step = 0, is_first = 1, and if armed (the reference's
+ *          `brain.loss != None`, :620) and reach_rate > threshold: complete = 1 (sticky, :644)
+ *   else:  step += 1, total_step += 1, is_first = 0                       (:681-682)
+ * Note the reference's quirks kept on purpose: the window counts every step (not episodes), and
+ * total_step does not count the step that ends an episode. */
+#define FFMP_EP_TOTALS 8  /* totals[]: env-steps, episodes, goals, collisions, truncations,
+                             completions, counted steps (sum of total_step increments), 0 */
+typedef struct ffmp_episode {
+  uint64_t* reach_bits; /* (N) bit k = is_goal k steps ago (bit 0 newest) */
+  int32_t* reach_len;   /* (N) flags in the window (<= window) */
+  double* reach_rate;   /* (N) */
+  int32_t* step;        /* (N) steps in the current episode */
+  int32_t* episode;     /* (N) episodes ended */
+  int64_t* total_step;  /* (N) */
+  uint8_t* is_first;    /* (N) 1 before the first step of an episode */
+  uint8_t* complete;    /* (N) sticky completion flag */
+  uint64_t* totals;     /* (FFMP_EP_TOTALS) running sums over all envs, or NULL */
+} ffmp_episode_t;
+
+/* Start (mask NULL: all envs) from the loop's initial values (:501-505): all counters 0,
+ * empty window, is_first = 1, complete = 0.  totals (if given) is zeroed when mask is NULL. */
+int ffmp_episode_init(int64_t n, const uint8_t* mask, ffmp_episode_t* ep, void* stream);
+/* One loop iteration for envs [0,n) from a step's flags (out.done, out.is_goal, out.collide,
+ * out.truncated; reward unused).  max_steps = 0 when out.done already includes truncation. */
+int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps,
+                        double threshold, int32_t armed, ffmp_episode_t* ep, void* stream);
 
 #ifdef __cplusplus
 }

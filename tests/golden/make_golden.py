@@ -16,6 +16,12 @@ What is driven (reference file:line):
     rospy: ROSNode.pi_to_pi (:167-172), relative_goal_calculator (:174-180),
     robot_velocity_calculator (:182-188), Environment.make_temporal_maps
     (:474-486).
+  * train.py main-loop episode bookkeeping (:579-587 reach_times / reach_rate,
+    :593 is_first, :606-607 truncation, :611-682 the is_done branch with its
+    episode / step / total_step counters and the reach-rate completion test),
+    compiled from the loop's own statements and driven with scripted
+    (is_goal, is_done) sequences; ROS, TensorBoard, CSV and torch.save are
+    inert stand-ins (unittest.mock), so only the bookkeeping runs.
 
 `gym` is not installed here (nor on the GPU box), so a minimal offline stand-in
 (this file's own code: Env, spaces.Box/Dict, envs.registration.register) is
@@ -33,6 +39,7 @@ import os
 import sys
 import tempfile
 import types
+import unittest.mock  # noqa: F401  (inert stand-ins for the loop's ROS / logging objects)
 
 import numpy as np
 
@@ -101,6 +108,53 @@ def _train_helpers():
     g = {"math": math, "np": np, "copy": copy, "torch": torch, "INPUT_CHANNELS": 2}
     exec(compile(mod, "<reference train.py helpers>", "exec"), g)
     return g
+
+
+def _episode_block():
+    """The bookkeeping statements of train.py's main loop, compiled from its AST."""
+    with open(os.path.join(REF_SRC, "train.py")) as f:
+        src = f.read()
+    tree = ast.parse(src)
+    loop = next(n for n in ast.walk(tree) if isinstance(n, ast.While) and "is_shutdown" in ast.unparse(n.test))
+    body = next(n for n in loop.body if isinstance(n, ast.If) and "is_start_callback_flag" in ast.unparse(n.test)).body
+
+    def keep(st):
+        txt = ast.unparse(st)
+        head = txt.splitlines()[0]
+        return (head in ("if is_goal:", "if len(reach_times) > REACH_MEMORY_CAPACITY:", "if step == MAX_STEPS:",
+                         "if is_done:", "is_first = False")
+                or head.startswith("train_env.reach_rate = "))
+
+    stmts = [st for st in body if keep(st)]
+    assert len(stmts) == 6, [ast.unparse(s_).splitlines()[0] for s_ in stmts]
+    return compile(ast.Module(body=stmts, type_ignores=[]), "<reference train.py episode bookkeeping>", "exec"), \
+        [st.lineno for st in stmts]
+
+
+def _run_episode_block(events, max_steps, armed):
+    """Drive the compiled bookkeeping with (is_goal, is_done) per loop iteration."""
+    from unittest import mock
+    code, _ = _episode_block()
+    train_env = mock.MagicMock()
+    train_env.agent.brain.loss = mock.MagicMock() if armed else None
+    g = {"np": np, "torch": mock.MagicMock(), "print": lambda *a, **k: None,
+         "MAX_STEPS": max_steps, "REACH_MEMORY_CAPACITY": 10, "REACH_RATE_THRESHOLD": 0.80,
+         "UPDATE_TARGET_EPISODE": 2, "MODEL_PATH": "/nonexistent/model.pth",
+         "ros": mock.MagicMock(), "tensor_board": mock.MagicMock(), "writer": mock.MagicMock(),
+         "train_env": train_env, "episode": 0, "step": 0, "total_step": 0, "reach_times": np.empty(0),
+         "is_first": True, "is_complete": False, "numpy_reward": 0.0, "reward": 0.0,
+         "relative_goal": np.zeros(2), "action_id": 3, "observe_m": None, "observe_g": None,
+         "observe_v": None, "observe_t": None}
+    rows = []
+    for goal, done in events:
+        first_in = g["is_first"]
+        g["is_goal"], g["is_done"] = bool(goal), bool(done)
+        exec(code, g)
+        rows.append({"is_goal": bool(goal), "is_done_in": bool(done), "first_in": bool(first_in),
+                     "reach_rate": float(train_env.reach_rate), "episode": int(g["episode"]),
+                     "step": int(g["step"]), "total_step": int(g["total_step"]),
+                     "is_complete": bool(g["is_complete"]), "is_first": bool(g["is_first"])})
+    return rows
 
 
 class _Pose(object):
@@ -309,6 +363,19 @@ def main():
             st = tenv.make_temporal_maps(frame, first)
         tm.append({"frame_value": float(k), "first": first, "stack": st[:, 0, 0].tolist(), "shape": list(st.shape)})
     out["temporal_maps"] = tm
+
+    # ---- train.py main-loop episode bookkeeping ----
+    ep = {"block_lines": _episode_block()[1], "window": 10, "threshold": 0.80, "scenarios": []}
+    for name, n, p_goal, p_col, max_steps, armed in (("mixed", 120, 0.15, 0.10, 6, True),
+                                                     ("goal_rich", 80, 0.85, 0.05, 6, True),
+                                                     ("goal_rich_unarmed", 60, 0.85, 0.05, 6, False),
+                                                     ("truncation_only", 40, 0.0, 0.0, 4, True),
+                                                     ("window_edge", 30, 0.5, 0.0, 200, True)):
+        u = rng.uniform(size=n)
+        events = [(bool(x < p_goal), bool(x < p_goal + p_col)) for x in u]
+        ep["scenarios"].append({"name": name, "max_steps": max_steps, "armed": armed,
+                                "rows": _run_episode_block(events, max_steps, armed)})
+    out["episode_bookkeeping"] = ep
 
     with open(os.path.join(OUT_DIR, "ref_pinned.json"), "w") as f:
         json.dump(out, f, indent=0, allow_nan=True)

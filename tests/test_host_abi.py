@@ -142,3 +142,20 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
+
+
+def test_episode_abi_validation_no_gpu(lib):
+    dummy = (C.c_double * 8)()
+    p = C.cast(dummy, C.c_void_p).value
+    ep = _abi.EpisodeT(*([p] * 9))
+    out = _abi.OutT(p, p, p, p, p)
+    assert lib.ffmp_episode_update(4, C.byref(out), 0, 0, 0.8, 1, C.byref(ep), None) == -1
+    assert b"window" in lib.ffmp_last_error()
+    assert lib.ffmp_episode_update(4, C.byref(out), 65, 0, 0.8, 1, C.byref(ep), None) == -1
+    assert lib.ffmp_episode_update(4, C.byref(out), 10, -1, 0.8, 1, C.byref(ep), None) == -1
+    assert lib.ffmp_episode_update(4, C.byref(_abi.OutT(p, p, None, p, p)), 10, 0, 0.8, 1, C.byref(ep), None) == -1
+    bad = _abi.EpisodeT(*([p] * 9))
+    bad.step = None
+    assert lib.ffmp_episode_init(4, None, C.byref(bad), None) == -1
+    assert lib.ffmp_episode_update(0, C.byref(out), 10, 0, 0.8, 1, C.byref(ep), None) == 0
+    assert lib.ffmp_episode_init(-1, None, C.byref(ep), None) == -1

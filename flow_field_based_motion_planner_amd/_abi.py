@@ -63,6 +63,7 @@ class EpisodeT(C.Structure):
 
 
 EP_TOTALS = 8
+EP_ARMED, EP_RESET_ITER = 1, 2
 
 
 def make_cfg(cfg: FFMPConfig, beam_cs_ptr: int = 0) -> CfgT:
@@ -106,7 +107,7 @@ _SIGS = {
     "ffmp_footprint_collision": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I64, _P, _P]),
     "ffmp_scan_collision": (C.c_int, [_I64, _I32, _P, C.c_double, _P, _P, _P]),
     "ffmp_scan_collision_f64": (C.c_int, [_I64, _I32, _P, C.c_double, _P, _P, _P]),
-    "ffmp_episode_init": (C.c_int, [_I64, _P, C.POINTER(EpisodeT), _P]),
+    "ffmp_episode_init": (C.c_int, [_I64, _P, _I32, C.POINTER(EpisodeT), _P]),
     "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
                                       _P]),
 }

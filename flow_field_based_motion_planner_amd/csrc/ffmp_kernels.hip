@@ -596,25 +596,29 @@ __device__ __forceinline__ void wave_count(uint64_t* totals, int k, bool pred) {
 }
 
 __global__ __launch_bounds__(256) void episode_init_kernel(int64_t n, const uint8_t* __restrict__ mask,
-                                                           ffmp_episode_t ep) {
+                                                           int32_t flags, ffmp_episode_t ep) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ep.totals && !mask && e < FFMP_EP_TOTALS) ep.totals[e] = 0;
-  if (e >= n || (mask && !mask[e])) return;
-  ep.reach_bits[e] = 0;
-  ep.reach_len[e] = 0;
-  ep.reach_rate[e] = 0.0;
-  ep.step[e] = 0;
-  ep.episode[e] = 0;
-  ep.total_step[e] = 0;
-  ep.is_first[e] = 1;
-  ep.complete[e] = 0;
+  const bool act = e < n && !(mask && !mask[e]);
+  const bool it0 = (flags & FFMP_EP_RESET_ITER) != 0;  // one (no-goal, not-done) iteration
+  if (act) {
+    ep.reach_bits[e] = 0;
+    ep.reach_len[e] = it0 ? 1 : 0;
+    ep.reach_rate[e] = 0.0;
+    ep.step[e] = it0 ? 1 : 0;
+    ep.episode[e] = 0;
+    ep.total_step[e] = it0 ? 1 : 0;
+    ep.is_first[e] = it0 ? 0 : 1;
+    ep.complete[e] = 0;
+  }
+  if (ep.totals) wave_count(ep.totals, 6, act && it0);
 }
 
 __global__ __launch_bounds__(256) void episode_update_kernel(int64_t n, ffmp_out_t out, int32_t window,
-                                                             int32_t max_steps, double threshold, int32_t armed,
+                                                             int32_t max_steps, double threshold, int32_t flags,
                                                              ffmp_episode_t ep) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = e < n;
+  const bool it0 = (flags & FFMP_EP_RESET_ITER) != 0;
   bool goal = false, done = false, trunc = false, col = false, fin = false;
   if (act) {
     goal = out.is_goal[e] != 0;
@@ -622,27 +626,36 @@ __global__ __launch_bounds__(256) void episode_update_kernel(int64_t n, ffmp_out
     const int32_t step = ep.step[e];
     // :579-587  reach_times.append(is_goal); keep the last REACH_MEMORY_CAPACITY; np.average
     const uint64_t keep = window >= 64 ? ~0ull : ((1ull << window) - 1ull);
-    const uint64_t bits = ((ep.reach_bits[e] << 1) | (goal ? 1ull : 0ull)) & keep;
-    const int32_t len = min(ep.reach_len[e] + 1, window);
-    const double rate = (double)__popcll(bits) / (double)len;
-    ep.reach_bits[e] = bits;
-    ep.reach_len[e] = len;
-    ep.reach_rate[e] = rate;
+    uint64_t bits = ((ep.reach_bits[e] << 1) | (goal ? 1ull : 0ull)) & keep;
+    int32_t len = min(ep.reach_len[e] + 1, window);
+    double rate = (double)__popcll(bits) / (double)len;
     // :607  if step == MAX_STEPS: is_done = True
     const bool own_trunc = max_steps > 0 && step == max_steps;
     done = (out.done[e] != 0) || own_trunc;
     trunc = done && ((out.truncated[e] != 0) || (own_trunc && !out.done[e]));
     if (done) {  // :611-663
       ep.episode[e] += 1;
-      ep.step[e] = 0;
-      ep.is_first[e] = 1;
-      fin = armed && rate > threshold;  // :644
+      fin = (flags & FFMP_EP_ARMED) && rate > threshold;  // :644
       if (fin) ep.complete[e] = 1;
+      if (it0) {  // the next episode's reset-observation iteration: no goal, not done
+        bits = (bits << 1) & keep;
+        len = min(len + 1, window);
+        rate = (double)__popcll(bits) / (double)len;
+        ep.step[e] = 1;
+        ep.total_step[e] += 1;
+        ep.is_first[e] = 0;
+      } else {
+        ep.step[e] = 0;
+        ep.is_first[e] = 1;
+      }
     } else {  // :593, :681-682
       ep.step[e] = step + 1;
       ep.total_step[e] += 1;
       ep.is_first[e] = 0;
     }
+    ep.reach_bits[e] = bits;
+    ep.reach_len[e] = len;
+    ep.reach_rate[e] = rate;
   }
   if (ep.totals) {
     wave_count(ep.totals, 0, act);
@@ -651,7 +664,7 @@ __global__ __launch_bounds__(256) void episode_update_kernel(int64_t n, ffmp_out
     wave_count(ep.totals, 3, col);
     wave_count(ep.totals, 4, trunc);
     wave_count(ep.totals, 5, fin);
-    wave_count(ep.totals, 6, act && !done);
+    wave_count(ep.totals, 6, act && (!done || it0));
   }
 }
 
@@ -884,17 +897,20 @@ int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double t
   return scan_impl<double>(n, L, ranges, thr, collide, min_r, stream);
 }
 
-int ffmp_episode_init(int64_t n, const uint8_t* mask, ffmp_episode_t* ep, void* stream) {
+int ffmp_episode_init(int64_t n, const uint8_t* mask, int32_t flags, ffmp_episode_t* ep, void* stream) {
   if (n < 0) return fail(FFMP_E_ARG, "negative n");
   if (const int rc = check_episode(ep)) return rc;
-  const int64_t m = n > FFMP_EP_TOTALS ? n : FFMP_EP_TOTALS;
-  hipLaunchKernelGGL(episode_init_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
-                     mask, *ep);
+  if (ep->totals && !mask &&
+      hipMemsetAsync(ep->totals, 0, sizeof(uint64_t) * FFMP_EP_TOTALS, (hipStream_t)stream) != hipSuccess)
+    return fail(FFMP_E_HIP, "ffmp_episode_init: hipMemsetAsync failed");
+  if (n == 0) return FFMP_OK;
+  hipLaunchKernelGGL(episode_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                     mask, flags, *ep);
   return check_launch("ffmp_episode_init");
 }
 
 int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps, double threshold,
-                        int32_t armed, ffmp_episode_t* ep, void* stream) {
+                        int32_t flags, ffmp_episode_t* ep, void* stream) {
   if (n < 0) return fail(FFMP_E_ARG, "negative n");
   if (window < 1 || window > 64) return fail(FFMP_E_ARG, "window must be in [1, 64], got %d", window);
   if (max_steps < 0) return fail(FFMP_E_ARG, "negative max_steps");
@@ -903,7 +919,7 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
   if (const int rc = check_episode(ep)) return rc;
   if (n == 0) return FFMP_OK;
   hipLaunchKernelGGL(episode_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     n, *out, window, max_steps, threshold, armed, *ep);
+                     n, *out, window, max_steps, threshold, flags, *ep);
   return check_launch("ffmp_episode_update");
 }
 

@@ -39,17 +39,22 @@ class EpisodeTracker:
             flag already includes truncation (FFMPVec does, at t == max_steps).
         armed: the reference only runs the completion test once a loss exists
             (train.py:620); set False until the learner has produced one.
+        reset_iteration: also run the loop's reset-observation iteration (the is_first
+            iteration that observes a freshly reset world, train.py:532-566) at start and after
+            every done, which a batched env folds into the resetting step.  True (default)
+            makes every counter equal the reference loop's for the same episodes; then
+            `step == env.t + 1`.  False counts env steps only (`step == env.t`).
     """
 
     def __init__(self, num_envs: int, window: int = 10, threshold: float = 0.80, max_steps: int = 0,
-                 armed: bool = True, device: Optional[torch.device] = None):
+                 armed: bool = True, reset_iteration: bool = True, device: Optional[torch.device] = None):
         if not 1 <= int(window) <= 64:
             raise ValueError(f"window must be in [1, 64], got {window}")
         if num_envs < 0 or max_steps < 0:
             raise ValueError("num_envs and max_steps must be >= 0")
         self.lib = _abi.load()
         self.num_envs, self.window, self.threshold = int(num_envs), int(window), float(threshold)
-        self.max_steps, self.armed = int(max_steps), bool(armed)
+        self.max_steps, self.armed, self.reset_iteration = int(max_steps), bool(armed), bool(reset_iteration)
         self.device = torch.device(device if device is not None else torch.cuda.current_device())
         if self.device.type != "cuda":
             raise _abi.FFMPBackendError("EpisodeTracker needs a GPU device (no CPU path)")
@@ -68,11 +73,15 @@ class EpisodeTracker:
             self.is_first, self.complete, self.totals)))
         self.init()
 
+    def _flags(self) -> int:
+        return (_abi.EP_ARMED if self.armed else 0) | (_abi.EP_RESET_ITER if self.reset_iteration else 0)
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def init(self, mask: Optional[torch.Tensor] = None) -> None:
-        """Loop start values (train.py:501-505) for the masked envs (all, and totals, if None)."""
+        """Loop start values (train.py:501-505) for the masked envs (all, and totals, if None),
+        followed by the reset-observation iteration when `reset_iteration`."""
         mp = None
         if mask is not None:
             mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
@@ -80,8 +89,8 @@ class EpisodeTracker:
                 raise ValueError("mask must have num_envs elements")
             mp = mask.data_ptr()
         with torch.cuda.device(self.device):
-            _abi.check(self.lib.ffmp_episode_init(self.num_envs, mp, C.byref(self._ep_c), self._stream()),
-                       "ffmp_episode_init")
+            _abi.check(self.lib.ffmp_episode_init(self.num_envs, mp, self._flags(), C.byref(self._ep_c),
+                                                  self._stream()), "ffmp_episode_init")
 
     def update(self, done: torch.Tensor, is_goal: torch.Tensor, collision: Optional[torch.Tensor] = None,
                truncated: Optional[torch.Tensor] = None) -> None:
@@ -101,7 +110,7 @@ class EpisodeTracker:
         out = _abi.OutT(None, *(t.data_ptr() for t in flags))
         with torch.cuda.device(self.device):
             _abi.check(self.lib.ffmp_episode_update(self.num_envs, C.byref(out), self.window, self.max_steps,
-                                                    self.threshold, int(self.armed), C.byref(self._ep_c),
+                                                    self.threshold, self._flags(), C.byref(self._ep_c),
                                                     self._stream()), "ffmp_episode_update")
 
     def update_from(self, env) -> None:

@@ -225,32 +225,39 @@ int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double t
  *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)
  *   reach_rate    =  np.average(window)                                    (:587, float64)
  *   done          =  out.done || (max_steps > 0 && step == max_steps)      (:607)
- *   done:  episode += 1, step = 0, is_first = 1, and if armed (the reference's
+ *   done:  episode += 1, step = 0, is_first = 1, and with FFMP_EP_ARMED (the reference's
  *          `brain.loss != None`, :620) and reach_rate > threshold: complete = 1 (sticky, :644)
  *   else:  step += 1, total_step += 1, is_first = 0                       (:681-682)
- * Note the reference's quirks kept on purpose: the window counts every step (not episodes), and
- * total_step does not count the step that ends an episode. */
-#define FFMP_EP_TOTALS 8  /* totals[]: env-steps, episodes, goals, collisions, truncations,
-                             completions, counted steps (sum of total_step increments), 0 */
+ * FFMP_EP_RESET_ITER: the reference loop spends one iteration observing each freshly reset world
+ * (is_first: never at the goal, never colliding) before an action takes effect; a batched env
+ * folds it into the step that resets.  With this flag that iteration is run here as well — in
+ * init and right after each done — so the counters equal the reference loop's.
+ * Kept on purpose: the window counts iterations (not episodes), and the iteration that ends an
+ * episode does not count towards total_step. */
+#define FFMP_EP_TOTALS 8  /* totals[]: env-steps (updates), episodes, goals, collisions,
+                             truncations, completions, counted steps (total_step increments), 0 */
+#define FFMP_EP_ARMED 1
+#define FFMP_EP_RESET_ITER 2
 typedef struct ffmp_episode {
-  uint64_t* reach_bits; /* (N) bit k = is_goal k steps ago (bit 0 newest) */
+  uint64_t* reach_bits; /* (N) bit k = is_goal k iterations ago (bit 0 newest) */
   int32_t* reach_len;   /* (N) flags in the window (<= window) */
   double* reach_rate;   /* (N) */
-  int32_t* step;        /* (N) steps in the current episode */
+  int32_t* step;        /* (N) iterations in the current episode */
   int32_t* episode;     /* (N) episodes ended */
   int64_t* total_step;  /* (N) */
-  uint8_t* is_first;    /* (N) 1 before the first step of an episode */
+  uint8_t* is_first;    /* (N) 1 before the first iteration of an episode */
   uint8_t* complete;    /* (N) sticky completion flag */
   uint64_t* totals;     /* (FFMP_EP_TOTALS) running sums over all envs, or NULL */
 } ffmp_episode_t;
 
-/* Start (mask NULL: all envs) from the loop's initial values (:501-505): all counters 0,
- * empty window, is_first = 1, complete = 0.  totals (if given) is zeroed when mask is NULL. */
-int ffmp_episode_init(int64_t n, const uint8_t* mask, ffmp_episode_t* ep, void* stream);
-/* One loop iteration for envs [0,n) from a step's flags (out.done, out.is_goal, out.collide,
+/* Start the masked envs (mask NULL: all, and totals zeroed) from the loop's initial values
+ * (:501-505: counters 0, empty window, is_first = 1, complete = 0), followed by the
+ * reset-observation iteration when flags has FFMP_EP_RESET_ITER. */
+int ffmp_episode_init(int64_t n, const uint8_t* mask, int32_t flags, ffmp_episode_t* ep, void* stream);
+/* One env step for envs [0,n) from its flags (out.done, out.is_goal, out.collide,
  * out.truncated; reward unused).  max_steps = 0 when out.done already includes truncation. */
 int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps,
-                        double threshold, int32_t armed, ffmp_episode_t* ep, void* stream);
+                        double threshold, int32_t flags, ffmp_episode_t* ep, void* stream);
 
 #ifdef __cplusplus
 }

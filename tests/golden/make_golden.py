@@ -131,8 +131,9 @@ def _episode_block():
         [st.lineno for st in stmts]
 
 
-def _run_episode_block(events, max_steps, armed):
-    """Drive the compiled bookkeeping with (is_goal, is_done) per loop iteration."""
+def _run_episode_block(events, max_steps, armed, n=None):
+    """Drive the compiled bookkeeping with (is_goal, is_done) per loop iteration; `events` is a
+    list, or a function of the previous iteration's row (None first) returning the next event."""
     from unittest import mock
     code, _ = _episode_block()
     train_env = mock.MagicMock()
@@ -146,7 +147,8 @@ def _run_episode_block(events, max_steps, armed):
          "relative_goal": np.zeros(2), "action_id": 3, "observe_m": None, "observe_g": None,
          "observe_v": None, "observe_t": None}
     rows = []
-    for goal, done in events:
+    seq = events if not callable(events) else (events(rows[-1] if rows else None) for _ in range(n))
+    for goal, done in seq:
         first_in = g["is_first"]
         g["is_goal"], g["is_done"] = bool(goal), bool(done)
         exec(code, g)
@@ -375,6 +377,20 @@ def main():
         events = [(bool(x < p_goal), bool(x < p_goal + p_col)) for x in u]
         ep["scenarios"].append({"name": name, "max_steps": max_steps, "armed": armed,
                                 "rows": _run_episode_block(events, max_steps, armed)})
+    # env-like streams: every episode starts with the iteration that observes the freshly reset
+    # world (never at the goal, never colliding), as in a simulator driven by this loop
+    for name, n, p_goal, p_col, max_steps in (("env_like", 150, 0.12, 0.08, 5), ("env_like_goals", 100, 0.6, 0.0, 9)):
+        def env_event(prev, p_goal=p_goal, p_col=p_col):
+            if prev is None or prev["is_first"]:  # the iteration that observes the reset world
+                return (False, False)
+            x = float(rng.uniform())
+            return (x < p_goal, x < p_goal + p_col)
+
+        rows = _run_episode_block(env_event, max_steps, True, n)
+        prev = 0
+        for r in rows:  # the iteration's final is_done (incl. the :607 truncation)
+            r["done_out"], prev = r["episode"] != prev, r["episode"]
+        ep["scenarios"].append({"name": name, "max_steps": max_steps, "armed": True, "env_like": True, "rows": rows})
     out["episode_bookkeeping"] = ep
 
     with open(os.path.join(OUT_DIR, "ref_pinned.json"), "w") as f:

@@ -86,3 +86,22 @@ def exact_report(g, o):
         same = (a == b) | (np.isnan(a) & np.isnan(b))
         out[k] = int((~same).sum())
     return out
+
+
+def env_like_stream(sc):
+    """Split an env-like golden scenario into env steps: [(row, state_row_after_update)], skipping
+    the reset-observation iterations (row 0 and each row after a done), which a batched env
+    folds into the step that resets; returns (initial_state_row, steps)."""
+    rows = sc["rows"]
+    steps, k = [], 1
+    while k < len(rows):
+        r = rows[k]
+        if r["done_out"]:
+            if k + 1 >= len(rows):
+                break
+            steps.append((r, rows[k + 1]))
+            k += 2
+        else:
+            steps.append((r, r))
+            k += 1
+    return rows[0], steps

@@ -156,6 +156,6 @@ def test_episode_abi_validation_no_gpu(lib):
     assert lib.ffmp_episode_update(4, C.byref(_abi.OutT(p, p, None, p, p)), 10, 0, 0.8, 1, C.byref(ep), None) == -1
     bad = _abi.EpisodeT(*([p] * 9))
     bad.step = None
-    assert lib.ffmp_episode_init(4, None, C.byref(bad), None) == -1
+    assert lib.ffmp_episode_init(4, None, 0, C.byref(bad), None) == -1
     assert lib.ffmp_episode_update(0, C.byref(out), 10, 0, 0.8, 1, C.byref(ep), None) == 0
-    assert lib.ffmp_episode_init(-1, None, C.byref(ep), None) == -1
+    assert lib.ffmp_episode_init(-1, None, 0, C.byref(ep), None) == -1

@@ -43,7 +43,7 @@ class CfgT(C.Structure):
 class StateT(C.Structure):
     _fields_ = [("pose", C.c_void_p), ("goal", C.c_void_p), ("d0", C.c_void_p), ("obst", C.c_void_p),
                 ("obst_r", C.c_void_p), ("t", C.c_void_p), ("episode", C.c_void_p), ("record", C.c_void_p),
-                ("err", C.c_void_p)]
+                ("err", C.c_void_p), ("term_record", C.c_void_p), ("term_obs", C.c_void_p)]
 
 
 class ObsT(C.Structure):

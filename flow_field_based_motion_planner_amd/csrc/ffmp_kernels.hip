@@ -111,6 +111,29 @@ FFMP_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One env's raster record: header, goal, then K float4 of each of cur / prev / vel.
+// Lane k writes obstacle k; lanes 0..3 the header words.
+FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const FrameHdr& hc, const FrameHdr& hp,
+                           float2 ge, float4 ecur, float4 eprev, float4 vel) {
+  if (lane == 0) {
+    rec[8] = ge.x;
+    rec[9] = ge.y;
+    rec[10] = 0.0f;
+    rec[11] = 0.0f;
+  }
+  if (lane < 4) {
+    rec[lane] = lane == 0 ? hc.px : lane == 1 ? hc.py : lane == 2 ? hc.c : hc.s;
+    rec[4 + lane] = lane == 0 ? hp.px : lane == 1 ? hp.py : lane == 2 ? hp.c : hp.s;
+    rec[12 + lane] = 0.0f;
+  }
+  if (has_obst) {
+    float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
+    ro[lane] = ecur;
+    ro[K + lane] = eprev;
+    ro[2 * K + lane] = vel;
+  }
+}
+
 template <int MODE, int kEnvWaves>
 __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                  const int64_t* __restrict__ action,
@@ -223,13 +246,21 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
     trunc = (cfg.max_steps > 0) && (t >= cfg.max_steps);
     done = col || goal || trunc;
     reset_now = done && cfg.autoreset;
-    if (!reset_now) {
+    if (lane == 0) {
       // small obs of the post-step state
-      if (lane == 0) {
-        ob.state_g[e * 2 + 0] = (float)dist;
-        ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
+      const float g0 = (float)dist, g1 = (float)pi_to_pi(atan2(dy, dx) - yaw1);
+      if (!reset_now) {
+        ob.state_g[e * 2 + 0] = g0;
+        ob.state_g[e * 2 + 1] = g1;
+      }
+      if (st.term_obs) {
+        float* to = st.term_obs + e * 5;
+        to[0] = g0; to[1] = g1; to[2] = (float)vlin; to[3] = (float)vang; to[4] = t_obs;
       }
     }
+    if (reset_now && st.term_record)  // the terminal state, before the reset below overwrites it
+      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev,
+                   to_ego(gx, gy, x1, y1, c1, s1), s_ecur[lane], s_eprev[lane], ego_vel(my, c1, s1));
   }
 
   if (reset_now) {
@@ -277,26 +308,16 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
       U = potential_cell(cfg, s_ecur, K, ge.x, ge.y, ic + di, ic + dj);
     }
     const float Uxp = __shfl(U, 0), Uxm = __shfl(U, 1), Uyp = __shfl(U, 2), Uym = __shfl(U, 3);
-    float* rec = st.record + e * rec_stride(K);
     if (lane == 0) {
       ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
       ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
-      rec[8] = ge.x;
-      rec[9] = ge.y;
-      rec[10] = 0.0f;
-      rec[11] = 0.0f;
     }
-    if (lane < 4) {
-      rec[lane] = lane == 0 ? hcur.px : lane == 1 ? hcur.py : lane == 2 ? hcur.c : hcur.s;
-      rec[4 + lane] = lane == 0 ? hprev.px : lane == 1 ? hprev.py : lane == 2 ? hprev.c : hprev.s;
-      rec[12 + lane] = 0.0f;
-    }
-    if (has_obst) {
-      float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
-      ro[lane] = s_ecur[lane];
-      ro[K + lane] = s_eprev[lane];
-      ro[2 * K + lane] = ego_vel(my, c1, s1);
-    }
+    const float4 ecur = has_obst ? s_ecur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 eprev = has_obst ? s_eprev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 vel = ego_vel(my, c1, s1);
+    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel);
+    if (MODE == kEnvMode_Step && !reset_now && st.term_record)
+      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel);
   }
 
   // ---- write back state / obs / outputs ----

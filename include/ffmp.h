@@ -111,6 +111,12 @@ typedef struct ffmp_state {
   int32_t* episode; /* (N)   episode counter (RNG key part)          */
   float* record;    /* (N, FFMP_REC_HDR + 12K) raster record */
   uint32_t* err;    /* (1)   sticky error bits (bit0: bad action id) */
+  /* Optional (NULL = not written): the post-step state of every env BEFORE auto-reset, i.e. what
+   * the reference loop observes on the iteration that ends an episode (train.py:543-557) —
+   * consumers that store transitions (a replay memory) need it for done envs. Written by
+   * ffmp_step / ffmp_step_state for all envs (equal to record / the small obs when not reset). */
+  float* term_record; /* (N, FFMP_REC_HDR + 12K) */
+  float* term_obs;    /* (N, 5) state_g[2], state_v[2], state_t */
 } ffmp_state_t;
 
 /* Observation tensors (device pointers).  Layout = reference train.py:44,543-557

@@ -1,0 +1,68 @@
+"""Network — the reference's dueling Q-network (src/train.py:231-303), batched on the GPU.
+
+Same layers, names and shapes as the reference, so its state_dict (and checkpoints, loaded
+with `torch.load(..., weights_only=True)`) load unchanged.  What changes is how the forward
+runs on a batch of env tensors already in HBM:
+
+  * no host round trips: the reference moves x_m / the tile / adv / val to the CPU and back
+    (:271-274, :296-300); here everything stays on the device;
+  * the fc1 "tile" (:261-267) is one gather: the loop `for i in range(grid_num): value =
+    x_gvt_[0][i]; tile = full((convw, convh), value)` keeps only its LAST value, i.e. feature
+    convw-1 of batch element 0, added to every cell of every channel of every sample.
+    `coupling="reference"` (default) reproduces that exactly, including the cross-sample
+    coupling at B > 1; `coupling="per_sample"` uses each sample's own feature, which is what
+    the reference computes for B = 1 (its acting path) and keeps samples independent.
+
+The convolutions and linears are plain library GEMMs (MIOpen / hipBLASLt through torch).
+Input maps must be G x G with G - 90 > 0 (conv k=32,32,8 then conv4 k=8 three times); the
+reference's fc2 (6400 inputs) fixes G = 100, other G size fc2 accordingly.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Network(nn.Module):
+    def __init__(self, input_channels: int = 2, outputs: int = 28, grid: int = 100, coupling: str = "reference"):
+        super().__init__()
+        if coupling not in ("reference", "per_sample"):
+            raise ValueError("coupling must be 'reference' or 'per_sample'")
+        side = grid - 31 - 31 - 7 - 3 * 7
+        if side <= 0:
+            raise ValueError(f"grid {grid} too small for the reference's convolution stack (needs > 90)")
+        conv3_side = grid - 31 - 31 - 7
+        if conv3_side > 67:
+            raise ValueError(f"grid {grid}: the fc1 tile reads feature {conv3_side - 1} of 67 (needs grid <= 136)")
+        self.coupling = coupling
+        self.grid = grid
+        self.conv1 = nn.Conv2d(input_channels, 32, kernel_size=32)
+        self.conv2 = nn.Conv2d(32, 64, kernel_size=32)
+        self.conv3 = nn.Conv2d(64, 64, kernel_size=8)
+        self.conv4 = nn.Conv2d(64, 64, kernel_size=8)
+        self.fc1 = nn.Linear(5, 67)
+        self.fc2 = nn.Linear(64 * side * side, 512)
+        self.fc3 = nn.Linear(512, 512)
+        self.fc4_ea = nn.Linear(512, outputs)  # A(s, a)
+        self.fc4_ev = nn.Linear(512, 1)        # V(s)
+
+    def forward(self, state_m: torch.Tensor, state_g: torch.Tensor, state_v: torch.Tensor,
+                state_t: torch.Tensor) -> torch.Tensor:
+        x_m = F.relu(self.conv1(state_m))
+        x_m = F.relu(self.conv2(x_m))
+        x_m = F.relu(self.conv3(x_m))
+        x_gvt = F.relu(self.fc1(torch.cat((state_g, state_v, state_t), 1)))
+        tile = x_gvt[:, x_m.shape[2] - 1]                      # the loop's last value (:263-267)
+        if self.coupling == "reference":
+            tile = tile[:1].expand(x_m.shape[0])               # x_gvt_[0][...]: batch element 0
+        x = x_m + tile.view(-1, 1, 1, 1)
+        x = F.relu(self.conv4(x))
+        x = F.relu(self.conv4(x))
+        x = F.relu(self.conv4(x))
+        x = torch.flatten(x, start_dim=1)
+        x = F.relu(self.fc2(x))
+        x = F.relu(self.fc3(x))
+        adv = self.fc4_ea(x)
+        val = self.fc4_ev(x)
+        return adv + val - adv.mean(1, keepdim=True).expand(-1, adv.size(1))

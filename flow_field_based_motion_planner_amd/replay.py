@@ -1,0 +1,170 @@
+"""ReplayMemory — a device-resident transition store for FFMPVec.
+
+The reference keeps a Python list of `Transition` namedtuples (src/train.py:44, 212-228),
+each holding two float32 (1,2,100,100) map stacks, and concatenates a minibatch on the host
+for every update (`Brain.make_minibatch`, :352-372).  Batched on one GPU that is ~1 MB per
+transition at 256² and a host round trip per sample.
+
+Here a transition is stored as what GENERATES its observations: the raster record of the
+state (the env's record before the step) and of the observation (its post-step record before
+auto-reset, `keep_terminal=True`), plus the small obs, action, reward and done —
+2 x (16 + 12K) + 10 floats + 13 B (1,717 B at C3, ~600x smaller than two f32 map stacks).
+`sample(B)` gathers B records of each kind and re-runs the raster kernel on them, producing
+the minibatch tensors in the reference's layout directly in HBM: bit-identical to the
+state_m / observe_m the env emitted (the raster is a pure function of the record).
+
+  ReplayMemory.push (:218-222)  -> push_begin(env) before env.step + push_end(env, action) after:
+                                   N transitions at slots index .. index+N-1 (mod capacity)
+  ReplayMemory.sample (:224-225) -> sample(B): uniform without replacement, like random.sample
+  ReplayMemory.__len__ (:227-228) -> len()
+  Brain.make_minibatch (:352-372) -> the returned Transition of batched tensors
+
+Transitions are causal: (obs_t, a_t, obs_t+1, r_t+1).  (The reference's asynchronous ROS loop
+pairs the action chosen from obs_t-1 with obs_t; a synchronous env has no such skew.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import namedtuple
+from typing import Optional, Tuple
+
+import torch
+
+from . import _abi
+
+# Field order of the reference's Transition (train.py:44)
+Transition = namedtuple("Transition", ("state_m", "state_g", "state_v", "state_t", "action", "observe_m",
+                                       "observe_g", "observe_v", "observe_t", "reward"))
+
+
+class ReplayMemory:
+    """Ring buffer of `capacity` transitions of `env` (an FFMPVec built with keep_terminal=True).
+
+    sample() materialises the map stacks with the env's raster kernel (state_m / observe_m
+    f32 (B,2,G,G); with `potential=True` also the potential planes (B,G,G) of both sides)."""
+
+    def __init__(self, env, capacity: int, seed: int = 0):
+        if not getattr(env, "keep_terminal", False):
+            raise ValueError("ReplayMemory needs FFMPVec(..., keep_terminal=True) (terminal records of done envs)")
+        if capacity < env.num_envs:
+            raise ValueError(f"capacity {capacity} < num_envs {env.num_envs}: one step would overwrite itself")
+        self.env, self.cfg, self.lib = env, env.cfg, env.lib
+        self.capacity = int(capacity)
+        self.device = env.device
+        R, dev = self.cfg.record_len(), self.device
+        self.s_record = torch.zeros(self.capacity, R, dtype=torch.float32, device=dev)
+        self.o_record = torch.zeros(self.capacity, R, dtype=torch.float32, device=dev)
+        self.s_small = torch.zeros(self.capacity, 5, dtype=torch.float32, device=dev)  # g[2], v[2], t
+        self.o_small = torch.zeros(self.capacity, 5, dtype=torch.float32, device=dev)
+        self.action = torch.zeros(self.capacity, dtype=torch.int64, device=dev)
+        self.reward = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(self.capacity, dtype=torch.bool, device=dev)
+        self.index = 0   # next slot (train.py:216)
+        self.size = 0    # len(self.memory)
+        self._pending = None
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(int(seed))
+        self._cfg_c = _abi.make_cfg(self.cfg, env.beam_cs.data_ptr() if env.beam_cs is not None else 0)
+        self._bufs = {}
+
+    def __len__(self) -> int:
+        return self.size
+
+    def hbm_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.s_record, self.o_record, self.s_small, self.o_small,
+                                                           self.action, self.reward, self.done))
+
+    # ----------------------------------------------------------------- push
+    def _slots(self, n: int):
+        a = self.index
+        first = min(n, self.capacity - a)
+        return [(a, 0, first)] + ([(0, first, n - first)] if first < n else [])
+
+    def push_begin(self, env=None) -> None:
+        """Before env.step(): record the current observation of every env as the transitions'
+        state (its raster record + state_g/state_v/state_t)."""
+        env = env or self.env
+        n = env.num_envs
+        small = torch.cat([env.state_g, env.state_v, env.state_t], dim=1)
+        for dst, src, cnt in self._slots(n):
+            self.s_record[dst:dst + cnt].copy_(env.record[src:src + cnt])
+            self.s_small[dst:dst + cnt].copy_(small[src:src + cnt])
+        self._pending = n
+
+    def push_end(self, action: torch.Tensor, env=None) -> None:
+        """After env.step(action): the observation (terminal state for envs that reset), action,
+        reward and done complete the N transitions; the ring index advances by N."""
+        env = env or self.env
+        n = env.num_envs
+        if self._pending != n:
+            raise RuntimeError("push_end() without a matching push_begin()")
+        action = torch.as_tensor(action, device=self.device).reshape(n).to(torch.int64)
+        for dst, src, cnt in self._slots(n):
+            self.o_record[dst:dst + cnt].copy_(env.term_record[src:src + cnt])
+            self.o_small[dst:dst + cnt].copy_(env.term_obs[src:src + cnt])
+            self.action[dst:dst + cnt].copy_(action[src:src + cnt])
+            self.reward[dst:dst + cnt].copy_(env.reward[src:src + cnt])
+            self.done[dst:dst + cnt].copy_(env.done[src:src + cnt])
+        self.index = (self.index + n) % self.capacity
+        self.size = min(self.size + n, self.capacity)
+        self._pending = None
+
+    # --------------------------------------------------------------- sample
+    def _batch_planes(self, key: str, B: int, potential: bool):
+        G = self.cfg.grid
+        want = (B, potential)
+        if self._bufs.get(key, (None,))[0] != want:
+            sm = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device)
+            pot = torch.empty(B, G, G, dtype=torch.float32, device=self.device) if potential else None
+            flow = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device) if self.cfg.flow else None
+            self._bufs[key] = (want, sm, pot, flow)
+        return self._bufs[key][1:]
+
+    def _raster(self, records: torch.Tensor, sm, pot, flow) -> None:
+        ob = _abi.ObsT(sm.data_ptr(), None, None, None, pot.data_ptr() if pot is not None else None, None, None,
+                       flow.data_ptr() if flow is not None else None)
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), records.shape[0], records.data_ptr(), None,
+                                               C.byref(ob), *self.env.raster_shape, stream), "ffmp_raster")
+
+    def sample_indices(self, batch_size: int, replacement: bool = False) -> torch.Tensor:
+        if batch_size > self.size and not replacement:
+            raise ValueError(f"sample larger than population ({batch_size} > {self.size})")  # as random.sample
+        if replacement:
+            return torch.randint(0, self.size, (batch_size,), generator=self.gen, device=self.device)
+        return torch.randperm(self.size, generator=self.gen, device=self.device)[:batch_size]
+
+    def sample(self, batch_size: int, replacement: bool = False, potential: bool = False,
+               index: Optional[torch.Tensor] = None) -> Tuple[Transition, dict]:
+        """A minibatch (Brain.make_minibatch layout) and extras {done, index[, potential,
+        observe_potential, flow, observe_flow]}.  The returned planes are reused by the next
+        sample() call of the same batch size (clone to keep them)."""
+        idx = self.sample_indices(batch_size, replacement) if index is None else index.to(self.device)
+        B = idx.numel()
+        s_rec = self.s_record.index_select(0, idx)
+        o_rec = self.o_record.index_select(0, idx)
+        s_sm, s_pot, s_flow = self._batch_planes("s", B, potential)
+        o_sm, o_pot, o_flow = self._batch_planes("o", B, potential)
+        self._raster(s_rec, s_sm, s_pot, s_flow)
+        self._raster(o_rec, o_sm, o_pot, o_flow)
+        ss = self.s_small.index_select(0, idx)
+        os_ = self.o_small.index_select(0, idx)
+        tr = Transition(s_sm, ss[:, 0:2], ss[:, 2:4], ss[:, 4:5], self.action.index_select(0, idx).view(B, 1),
+                        o_sm, os_[:, 0:2], os_[:, 2:4], os_[:, 4:5], self.reward.index_select(0, idx))
+        extra = {"done": self.done.index_select(0, idx), "index": idx}
+        if potential:
+            extra["potential"], extra["observe_potential"] = s_pot, o_pot
+        if self.cfg.flow:
+            extra["flow"], extra["observe_flow"] = s_flow, o_flow
+        return tr, extra
+
+    def state_dict(self) -> dict:
+        return {"s_record": self.s_record.clone(), "o_record": self.o_record.clone(), "s_small": self.s_small.clone(),
+                "o_small": self.o_small.clone(), "action": self.action.clone(), "reward": self.reward.clone(),
+                "done": self.done.clone(), "index": self.index, "size": self.size}
+
+    def load_state_dict(self, sd: dict) -> None:
+        for k in ("s_record", "o_record", "s_small", "o_small", "action", "reward", "done"):
+            getattr(self, k).copy_(sd[k])
+        self.index, self.size = int(sd["index"]), int(sd["size"])

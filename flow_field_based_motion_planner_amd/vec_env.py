@@ -45,12 +45,15 @@ class FFMPVec:
         env_offset: global index of env 0 (shard start); RNG streams are keyed
             by the global index so trajectories do not depend on sharding.
         potential: also raster the potential plane (default True).
+        keep_terminal: also keep every env's post-step state before auto-reset
+            (`term_record` (N, record_len) and `term_obs` (N, 5) = state_g, state_v, state_t):
+            what a transition store needs for envs that just finished (ReplayMemory).
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
-                 autotune: bool = True, pipeline: Optional[int] = None):
+                 autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -70,6 +73,7 @@ class FFMPVec:
         self.env_offset = int(env_offset)
         self.with_potential = bool(potential)
         self.arena = bool(arena)
+        self.keep_terminal = bool(keep_terminal)
         self.placement = None
         self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
         self._alloc()
@@ -109,6 +113,8 @@ class FFMPVec:
             ("grad", (N, 2), f32), ("lidar", (N, L), f32),
             ("reward", (N,), f32), ("done", (N,), b), ("is_goal", (N,), b), ("collision", (N,), b),
             ("truncated", (N,), b),
+            # optional: post-step state before auto-reset (ffmp_state_t.term_*)
+            ("term_record", (N, cfg.record_len()), f32), ("term_obs", (N, 5), f32),
         ]
         if not self.with_potential:
             specs = [sp for sp in specs if sp[0] != "potential"]
@@ -116,6 +122,8 @@ class FFMPVec:
             specs = [sp for sp in specs if sp[0] != "flow"]
         if L == 0:
             specs = [sp for sp in specs if sp[0] != "lidar"]
+        if not self.keep_terminal:
+            specs = [sp for sp in specs if not sp[0].startswith("term_")]
         return specs
 
     def _alloc(self):
@@ -126,6 +134,8 @@ class FFMPVec:
         self.potential = None
         self.lidar = None
         self.flow = None
+        self.term_record = None
+        self.term_obs = None
         if self.arena:
             self._arena_offs, off = [], 0
             for _, shape, dtype in specs:
@@ -247,7 +257,8 @@ class FFMPVec:
         self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
         self._state_c = _abi.StateT(self.pose.data_ptr(), self.goal.data_ptr(), self.d0.data_ptr(),
                                     self.obst.data_ptr(), self.obst_r.data_ptr(), self.t.data_ptr(),
-                                    self.episode.data_ptr(), self.record.data_ptr(), self.err.data_ptr())
+                                    self.episode.data_ptr(), self.record.data_ptr(), self.err.data_ptr(),
+                                    _ptr(self.term_record), _ptr(self.term_obs))
         self._obs_c = _abi.ObsT(self.state_m.data_ptr(), self.state_g.data_ptr(), self.state_v.data_ptr(),
                                 self.state_t.data_ptr(), _ptr(self.potential), self.grad.data_ptr(),
                                 _ptr(self.lidar), _ptr(self.flow))
@@ -272,7 +283,7 @@ class FFMPVec:
             a, n = bounds[k], bounds[k + 1] - bounds[k]
             st = _abi.StateT(off(self.pose, a), off(self.goal, a), off(self.d0, a), off(self.obst, a),
                              off(self.obst_r, a), off(self.t, a), off(self.episode, a), off(self.record, a),
-                             self.err.data_ptr())
+                             self.err.data_ptr(), off(self.term_record, a), off(self.term_obs, a))
             ob = _abi.ObsT(off(self.state_m, a), off(self.state_g, a), off(self.state_v, a), off(self.state_t, a),
                            off(self.potential, a), off(self.grad, a), off(self.lidar, a), off(self.flow, a))
             out = _abi.OutT(off(self.reward, a), off(self.done, a), off(self.is_goal, a), off(self.collision, a),

@@ -76,7 +76,8 @@ int main(void) {
   const size_t G2 = (size_t)G * G, rec = FFMP_REC_HDR + 12 * K;
   ffmp_state_t st = {(double*)dalloc(N * 3 * 8), (double*)dalloc(N * 2 * 8), (double*)dalloc(N * 8),
                      (double*)dalloc(N * K * 4 * 8), (double*)dalloc(N * K * 8), (int32_t*)dalloc(N * 4),
-                     (int32_t*)dalloc(N * 4), (float*)dalloc(N * rec * 4), (uint32_t*)dalloc(4)};
+                     (int32_t*)dalloc(N * 4), (float*)dalloc(N * rec * 4), (uint32_t*)dalloc(4),
+                     NULL, NULL /* no terminal record / obs */};
   ffmp_obs_t ob = {(float*)dalloc(N * 2 * G2 * 4), (float*)dalloc(N * 2 * 4), (float*)dalloc(N * 2 * 4),
                    (float*)dalloc(N * 4), (float*)dalloc(N * G2 * 4), (float*)dalloc(N * 2 * 4),
                    (float*)dalloc(N * L * 4), NULL};

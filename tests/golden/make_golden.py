@@ -16,6 +16,9 @@ What is driven (reference file:line):
     rospy: ROSNode.pi_to_pi (:167-172), relative_goal_calculator (:174-180),
     robot_velocity_calculator (:182-188), Environment.make_temporal_maps
     (:474-486).
+  * train.py Network (:231-303), compiled from the AST and run on CPU with deterministic
+    numpy weights (tests/parity_util.network_weights) on synthetic G=100 inputs at B=1 and B=3
+    (B>1 pins the batch coupling of the fc1 tile, :261-267).
   * train.py main-loop episode bookkeeping (:579-587 reach_times / reach_rate,
     :593 is_first, :606-607 truncation, :611-682 the is_done branch with its
     episode / step / total_step counters and the reach-rate completion test),
@@ -157,6 +160,33 @@ def _run_episode_block(events, max_steps, armed, n=None):
                      "step": int(g["step"]), "total_step": int(g["total_step"]),
                      "is_complete": bool(g["is_complete"]), "is_first": bool(g["is_first"])})
     return rows
+
+
+def _network_outputs(out, maps):
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT_DIR)))
+    from tests.parity_util import network_inputs, network_weights
+    with open(os.path.join(REF_SRC, "train.py")) as f:
+        tree = ast.parse(f.read())
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Network")
+    g = {"torch": torch, "nn": nn, "F": F, "BATCH_SIZE": 1024, "device": torch.device("cpu")}
+    exec(compile(ast.Module(body=[cls], type_ignores=[]), "<reference train.py Network>", "exec"), g)
+    torch.manual_seed(0)
+    net = g["Network"](2, 28)
+    sd = net.state_dict()
+    w = network_weights([(k, tuple(v.shape)) for k, v in sd.items()])
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    net.eval()
+    res = {"weights": "tests/parity_util.network_weights(seed=1234)", "param_shapes": [[k, list(v.shape)] for k, v in
+                                                                                       sd.items()], "cases": []}
+    for batch, seed in ((1, 71), (3, 72), (2, 73)):
+        sm, gg, vv, tt = network_inputs(batch, seed)
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            q = net(torch.from_numpy(sm), torch.from_numpy(gg), torch.from_numpy(vv), torch.from_numpy(tt))
+        res["cases"].append({"batch": batch, "seed": seed, "q": q.numpy().astype(float).tolist()})
+    out["network"] = res
 
 
 class _Pose(object):
@@ -365,6 +395,9 @@ def main():
             st = tenv.make_temporal_maps(frame, first)
         tm.append({"frame_value": float(k), "first": first, "stack": st[:, 0, 0].tolist(), "shape": list(st.shape)})
     out["temporal_maps"] = tm
+
+    # ---- train.py Network ----
+    _network_outputs(out, maps)
 
     # ---- train.py main-loop episode bookkeeping ----
     ep = {"block_lines": _episode_block()[1], "window": 10, "threshold": 0.80, "scenarios": []}

@@ -17,6 +17,9 @@ def gpu_snapshot(env, sl=slice(None)):
     d["potential"] = env.potential[sl].detach().cpu().numpy() if env.potential is not None else None
     d["lidar"] = env.lidar[sl].detach().cpu().numpy() if env.lidar is not None else None
     d["flow"] = env.flow[sl].detach().cpu().numpy() if env.flow is not None else None
+    for k in ("term_record", "term_obs"):
+        t = getattr(env, k, None)
+        d[k] = t[sl].detach().cpu().numpy() if t is not None else None
     K = env.cfg.n_obst
     if K == 0:
         d["obst"] = d["obst"][:, :0]
@@ -31,6 +34,8 @@ def oracle_snapshot(ref):
     d["potential"] = ref.potential if ref.with_potential else None
     d["lidar"] = ref.lidar if ref.cfg.n_beams else None
     d["flow"] = ref.flow
+    d["term_record"] = getattr(ref, "term_record", None)
+    d["term_obs"] = getattr(ref, "term_obs", None)
     return d
 
 
@@ -50,6 +55,13 @@ def compare(g, o, where=""):
         bad.append(f"{where} flow: present on one side only")
     elif g.get("flow") is not None and not np.array_equal(g["flow"], o["flow"]):
         bad.append(f"{where} flow: {int((g['flow'] != o['flow']).sum())} elements differ")
+    if g.get("term_record") is not None:  # only envs built with keep_terminal have them
+        c = diff_count(g["term_record"], o["term_record"])
+        if c:
+            bad.append(f"{where} term_record: {c} elements differ")
+        a, b = np.asarray(g["term_obs"], dtype=np.float64), np.asarray(o["term_obs"], dtype=np.float64)
+        if a.shape != b.shape or not np.allclose(a, b, rtol=0, atol=F32_OBS_ATOL):
+            bad.append(f"{where} term_obs: mismatch")
     for k in EXACT_FIELDS + ("record",):
         c = diff_count(g[k], o[k])
         if c:
@@ -105,3 +117,37 @@ def env_like_stream(sc):
             steps.append((r, r))
             k += 1
     return rows[0], steps
+
+
+def network_weights(shapes, seed=1234):
+    """Deterministic float32 weights for the reference Network (name -> array), in state_dict
+    order: weights ~ N(0, 1/fan_in), biases ~ N(0, 0.05^2).  numpy-only so the golden script and
+    the GPU test build the same values on any machine."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, shape in shapes:
+        if name.endswith("weight"):
+            fan_in = int(np.prod(shape[1:]))
+            out[name] = (rng.standard_normal(shape) / np.sqrt(fan_in)).astype(np.float32)
+        else:
+            out[name] = (rng.standard_normal(shape) * 0.05).astype(np.float32)
+    return out
+
+
+def network_inputs(batch, seed):
+    """Synthetic Network inputs at the reference map size (G=100): two 0/255 occupancy frames of
+    random discs, relative goal, velocity and dt."""
+    rng = np.random.default_rng(seed)
+    G = 100
+    yy, xx = np.mgrid[0:G, 0:G]
+    sm = np.zeros((batch, 2, G, G), dtype=np.float32)
+    for b in range(batch):
+        for f in range(2):
+            for _ in range(int(rng.integers(3, 9))):
+                cx, cy, r = rng.uniform(0, G), rng.uniform(0, G), rng.uniform(2, 9)
+                sm[b, f][(xx - cx) ** 2 + (yy - cy) ** 2 <= r * r] = 255.0
+    g = np.stack([rng.uniform(0.5, 5.0, batch), rng.uniform(-np.pi, np.pi, batch)], 1).astype(np.float32)
+    v = np.stack([rng.uniform(0, 0.06, batch), rng.uniform(-0.06, 0.06, batch)], 1).astype(np.float32)
+    t = rng.uniform(0.0, 0.2, (batch, 1)).astype(np.float32)
+    return sm, g, v, t
+

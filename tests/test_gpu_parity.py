@@ -30,8 +30,8 @@ CASES = {
 }
 
 
-def _run(cfg, n, steps, seed=0, env_offset=0):
-    env = FFMPVec(n, cfg, device="cuda:0", env_offset=env_offset)
+def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True):
+    env = FFMPVec(n, cfg, device="cuda:0", env_offset=env_offset, keep_terminal=keep_terminal)
     ref = OracleVecEnv(cfg, n, env_offset=env_offset)
     env.reset()
     ref.reset()
@@ -56,7 +56,7 @@ def _run(cfg, n, steps, seed=0, env_offset=0):
 @pytest.mark.parametrize("name", list(CASES))
 def test_step_parity(name):
     cfg, n, steps = CASES[name]
-    env, ref, problems, counts = _run(cfg, n, steps)
+    env, ref, problems, counts = _run(cfg, n, steps, keep_terminal=name != "C2_128_static")
     assert not problems, "\n".join(problems[:20])
     if name == "dense_collisions":
         assert counts["collision"] > 0 and counts["done"] > 0, counts  # the reset path is exercised

@@ -1,0 +1,68 @@
+"""Batched Network (network.py) against the reference Network (src/train.py:231-303) run by
+tests/golden/make_golden.py on the same deterministic weights and inputs (golden "network").
+CPU: float32 torch on the host (the learner is a torch consumer, not a HIP kernel);
+GPU: the same on cuda:0, where MIOpen's convolution algorithms reorder the float32 sums."""
+import numpy as np
+import pytest
+import torch
+
+from flow_field_based_motion_planner_amd.network import Network
+from tests.parity_util import network_inputs, network_weights
+
+# |q| ~ 10; float32 sums over up to 32,768 products per output of conv2
+CPU_ATOL, GPU_ATOL, RTOL = 1e-4, 2e-3, 1e-4
+
+
+def _net(golden, device, coupling="reference"):
+    net = Network(2, 28, grid=100, coupling=coupling)
+    shapes = [(k, tuple(v)) for k, v in golden["network"]["param_shapes"]]
+    assert [(k, tuple(v.shape)) for k, v in net.state_dict().items()] == shapes
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in network_weights(shapes).items()})
+    return net.to(device).eval()
+
+
+def _inputs(case, device):
+    return [torch.from_numpy(x).to(device) for x in network_inputs(case["batch"], case["seed"])]
+
+
+def _check(golden, device, atol):
+    net = _net(golden, device)
+    for case in golden["network"]["cases"]:
+        with torch.no_grad():
+            q = net(*_inputs(case, device)).cpu().numpy()
+        want = np.asarray(case["q"], dtype=np.float32)
+        assert q.shape == want.shape
+        np.testing.assert_allclose(q, want, rtol=RTOL, atol=atol, err_msg=f"batch {case['batch']}")
+
+
+def test_reference_outputs_cpu(golden):
+    _check(golden, "cpu", CPU_ATOL)
+
+
+def test_per_sample_coupling_cpu(golden):
+    """per_sample == running each sample alone (the reference's B=1 result), and differs from
+    the reference coupling at B>1."""
+    ref = _net(golden, "cpu")
+    per = _net(golden, "cpu", coupling="per_sample")
+    case = next(c for c in golden["network"]["cases"] if c["batch"] == 3)
+    sm, g, v, t = _inputs(case, "cpu")
+    with torch.no_grad():
+        batched = per(sm, g, v, t)
+        alone = torch.cat([ref(sm[i:i + 1], g[i:i + 1], v[i:i + 1], t[i:i + 1]) for i in range(3)])
+        coupled = ref(sm, g, v, t)
+    torch.testing.assert_close(batched, alone, rtol=1e-5, atol=1e-4)
+    assert not torch.allclose(coupled[1:], alone[1:], atol=1e-3)
+    torch.testing.assert_close(coupled[:1], alone[:1], rtol=1e-5, atol=1e-4)
+
+
+def test_grid_validation():
+    with pytest.raises(ValueError):
+        Network(grid=64)
+    with pytest.raises(ValueError):
+        Network(grid=256)
+    assert Network(grid=128).fc2.in_features == 64 * 38 * 38
+
+
+@pytest.mark.gpu
+def test_reference_outputs_gpu(golden):
+    _check(golden, "cuda:0", GPU_ATOL)

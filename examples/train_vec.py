@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""train.py's main loop (src/train.py:523-693) on the batched env, entirely on one GPU.
+
+    reference                                   here
+    ROS callbacks -> observe_* (:532-557)       obs = env.step(...) (device tensors, in place)
+    agent.get_action (:572)                     brain.decide_action(obs, episode) for all envs
+    rewarder2 + reach_times (:577-587)          env flags -> tracker.update_from(env)
+    agent.memorize (:596)                       brain.memory.push_begin/push_end around the step
+    agent.update_q_function (:597)              brain.replay() every --replay-every steps
+    update_target every 2 episodes (:636-637)   every --target-every replays
+    reach_rate > 0.8 -> save (:644-648)         tracker.summary()["any_complete"]
+
+Usage: python examples/train_vec.py --envs 1024 --steps 300
+Prints one JSON line: env-steps/s of the whole loop, learner updates, losses, episode totals.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from flow_field_based_motion_planner_amd import EpisodeTracker, FFMPConfig  # noqa: E402
+from flow_field_based_motion_planner_amd.learner import Brain  # noqa: E402
+from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--batch", type=int, default=1024)        # BATCH_SIZE, train.py:62
+    ap.add_argument("--capacity", type=int, default=200_000)
+    ap.add_argument("--replay-every", type=int, default=1)
+    ap.add_argument("--target-every", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save", default="")
+    args = ap.parse_args()
+
+    dev = torch.device("cuda:0")
+    # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
+    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed)
+    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True)
+    brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed)
+    obs = env.reset()
+    tracker = EpisodeTracker(args.envs, device=dev)
+    losses, updates = [], 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        action = brain.decide_action(obs, tracker.episode)
+        brain.memory.push_begin()
+        obs, reward, done, info = env.step(action)
+        brain.memory.push_end(action)
+        tracker.update_from(env)
+        if step % args.replay_every == 0:
+            loss = brain.replay()
+            if loss is not None:
+                updates += 1
+                if updates % 20 == 1:
+                    losses.append(float(loss))
+                if updates % args.target_every == 0:
+                    brain.update_target_q_network()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    env.check_errors()
+    summ = tracker.summary()
+    out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "envs": args.envs, "steps": args.steps,
+           "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],
+           "replay_bytes": brain.memory.hbm_bytes(), "replay_len": len(brain.memory), **summ}
+    print(json.dumps(out))
+    if args.save:
+        torch.save(brain.main_q_network.state_dict(), args.save)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+"""Brain — the reference's double-DQN learner (src/train.py:306-431), batched over FFMPVec envs.
+
+Everything stays in HBM: transitions go into the device ReplayMemory (records), minibatches
+are re-rastered there, and the Q-networks run on the batch without host round trips.
+
+  Brain.__init__ (:307-314)                     -> same hyper-parameters (train.py:57-79)
+  Brain.decide_action (:337-349)                -> decide_action(obs, episode): per-env
+      epsilon = 0.5 * (1 / (episode + 1)); greedy iff epsilon <= U(0,1); batched, per_sample
+      coupling (= the reference's B = 1 forward for every env)
+  Brain.replay (:316-334) + make_minibatch (:352-372)
+      + get_expected_state_action_values (:374-412) + update_main_q_network (:414-428)
+                                                -> replay(): sample, Q(s,a), a* = argmax_a
+      Q_main(s',a), y = r + GAMMA * Q_target(s', a*) (no terminal mask, as the reference;
+      mask_terminal=True multiplies by 1 - done), MSE, Adam step
+  Brain.update_target_q_network (:430-431)      -> same
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from .network import Network
+from .replay import ReplayMemory
+
+GAMMA = 0.95            # train.py:57
+BATCH_SIZE = 1024       # train.py:62
+CAPACITY = 20000        # train.py:64
+LEARNING_RATE = 0.0005  # train.py:70
+NUM_ACTIONS = 28        # train.py:69
+INPUT_CHANNELS = 2      # train.py:68
+
+
+class Brain:
+    def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
+                 lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
+                 seed: int = 0):
+        self.env = env
+        self.device = env.device
+        self.num_actions = NUM_ACTIONS
+        self.batch_size, self.gamma, self.mask_terminal = int(batch_size), float(gamma), bool(mask_terminal)
+        self.replay_coupling = replay_coupling
+        self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed)
+        g = env.cfg.grid
+        with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
+            torch.manual_seed(seed)
+            self.main_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
+            self.target_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
+        self.optimizer = torch.optim.Adam(self.main_q_network.parameters(), lr=lr)
+        self.loss: Optional[torch.Tensor] = None
+        self.step = 0
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seed) + 1)
+
+    @staticmethod
+    def _q(net: Network, coupling: str, sm, sg, sv, st):
+        prev, net.coupling = net.coupling, coupling
+        try:
+            return net(sm, sg, sv, st)
+        finally:
+            net.coupling = prev
+
+    def decide_action(self, obs: Dict[str, torch.Tensor], episode: torch.Tensor) -> torch.Tensor:
+        """Epsilon-greedy actions (N,) int64 for every env (train.py:337-349)."""
+        n = obs["state_m"].shape[0]
+        epsilon = 0.5 * (1.0 / (episode.to(torch.float64) + 1.0))
+        u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
+        self.main_q_network.eval()
+        with torch.no_grad():
+            q = self._q(self.main_q_network, "per_sample", obs["state_m"], obs["state_g"], obs["state_v"],
+                        obs["state_t"])
+        greedy = q.max(1)[1]
+        rand = torch.randint(0, self.num_actions, (n,), generator=self.gen, device=self.device)
+        return torch.where(epsilon <= u, greedy, rand)
+
+    def replay(self, index: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """One learner update; None until the memory holds a minibatch (train.py:319-320)."""
+        if len(self.memory) < self.batch_size and index is None:
+            return None
+        b, ex = self.memory.sample(self.batch_size, index=index)
+        c = self.replay_coupling
+        self.main_q_network.eval()
+        self.target_q_network.eval()
+        sav = self._q(self.main_q_network, c, b.state_m, b.state_g, b.state_v, b.state_t).gather(1, b.action)
+        with torch.no_grad():
+            a_m = self._q(self.main_q_network, c, b.observe_m, b.observe_g, b.observe_v, b.observe_t).max(1)[1]
+            nxt = self._q(self.target_q_network, c, b.observe_m, b.observe_g, b.observe_v,
+                          b.observe_t).gather(1, a_m.view(-1, 1)).squeeze(1)
+            if self.mask_terminal:
+                nxt = nxt * (~ex["done"]).to(nxt.dtype)
+            expected = b.reward + self.gamma * nxt
+        self.main_q_network.train()
+        loss = nn.functional.mse_loss(sav, expected.unsqueeze(1))
+        self.loss = loss
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+        return loss.detach()
+
+    def update_target_q_network(self) -> None:
+        self.target_q_network.load_state_dict(self.main_q_network.state_dict())

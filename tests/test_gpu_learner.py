@@ -1,0 +1,88 @@
+"""Batched learner (learner.Brain) on env tensors: one replay() update equals the reference
+Brain's arithmetic (src/train.py:352-428, restated below on copies of the networks), and
+decide_action follows the epsilon-greedy rule of :337-349.  The reference Brain itself needs
+CUDA tensor types (torch.cuda.ByteTensor / LongTensor), so it is not run here: this
+parity is against its restated formulas."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from flow_field_based_motion_planner_amd import FFMPConfig
+from flow_field_based_motion_planner_amd.learner import Brain
+from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _env(n=32):
+    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=64, moving=True, max_steps=6, seed=31)
+    env = FFMPVec(n, cfg, device=DEV, keep_terminal=True)
+    env.reset()
+    return env
+
+
+def _fill(brain, env, steps):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for _ in range(steps):
+        brain.memory.push_begin()
+        a = torch.randint(0, 28, (env.num_envs,), generator=g).to(DEV)
+        env.step(a)
+        brain.memory.push_end(a)
+
+
+def test_replay_update_matches_reference_formulas():
+    env = _env()
+    brain = Brain(env, capacity=256, batch_size=48, seed=3)
+    assert brain.replay() is None  # train.py:319-320: not enough memory yet
+    _fill(brain, env, 3)
+    idx = torch.randperm(len(brain.memory), device=DEV)[:48]
+    main0 = copy.deepcopy(brain.main_q_network)
+    targ0 = copy.deepcopy(brain.target_q_network)
+    opt0 = torch.optim.Adam(main0.parameters(), lr=0.0005)
+    b, ex = brain.memory.sample(48, index=idx)
+    b = type(b)(*[t.clone() for t in b])
+    loss = brain.replay(index=idx)
+    # reference arithmetic (get_expected_state_action_values + update_main_q_network)
+    main0.eval()
+    targ0.eval()
+    sav = main0(b.state_m, b.state_g, b.state_v, b.state_t).gather(1, b.action)
+    a_m = main0(b.observe_m, b.observe_g, b.observe_v, b.observe_t).detach().max(1)[1].view(-1, 1)
+    nxt = targ0(b.observe_m, b.observe_g, b.observe_v, b.observe_t).gather(1, a_m).detach().squeeze()
+    expected = (b.reward.cpu() + 0.95 * nxt.cpu()).to(DEV)
+    main0.train()
+    ref_loss = nn.MSELoss()(sav, expected.unsqueeze(1))
+    opt0.zero_grad()
+    ref_loss.backward()
+    opt0.step()
+    torch.testing.assert_close(loss, ref_loss.detach(), rtol=1e-5, atol=1e-5)
+    # gradients agree to float32 reduction-order noise (MIOpen may pick different backward
+    # algorithms for two identical calls); Adam's first step moves every parameter by at most
+    # ~lr in the direction of sign(grad), so parameters agree within 2*lr and mostly far closer
+    for (k, p), (_, q) in zip(brain.main_q_network.named_parameters(), main0.named_parameters()):
+        gmax = float(q.grad.abs().max())
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-3, atol=1e-4 * gmax + 1e-12, msg=k)
+        d = (p - q).abs()
+        assert float(d.max()) <= 2 * 0.0005 + 1e-6, k
+        assert float((d <= 1e-6).float().mean()) > 0.9, k
+    brain.update_target_q_network()
+    for p, q in zip(brain.main_q_network.parameters(), brain.target_q_network.parameters()):
+        assert torch.equal(p, q)
+
+
+def test_decide_action_epsilon_greedy():
+    env = _env(256)
+    brain = Brain(env, capacity=512, batch_size=32, seed=4)
+    obs = env.obs
+    brain.main_q_network.eval()
+    with torch.no_grad():
+        greedy = torch.cat([brain.main_q_network(obs["state_m"][i:i + 1], obs["state_g"][i:i + 1],
+                                                 obs["state_v"][i:i + 1], obs["state_t"][i:i + 1]).max(1)[1]
+                            for i in range(256)])
+    late = brain.decide_action(obs, torch.full((256,), 10 ** 9, device=DEV))
+    assert torch.equal(late, greedy)  # epsilon ~ 0: always greedy, per-env B=1 semantics
+    first = brain.decide_action(obs, torch.zeros(256, dtype=torch.int32, device=DEV))  # epsilon 0.5
+    frac = float((first != greedy).float().mean())
+    assert 0.3 < frac < 0.65 and first.dtype == torch.int64 and int(first.max()) < 28

@@ -3,7 +3,8 @@
 
 One "step" = one FFMPVec step of every env this rank owns: the env kernel
 (integrate, obstacles, lidar, collision/reward/done, auto-reset) + the raster
-kernel (both float32 frames of state_m and the float32 potential plane).
+kernel (the new float32 frame of the state_m temporal stack — both frames when
+the frame window wraps or an env resets — and the float32 potential plane).
 Actions for every timed step are pre-generated on the device (inputs resident
 in HBM before the timed region).
 
@@ -43,6 +44,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
+    p.add_argument("--frame-window", type=int, default=None,
+                   help="frames per env kept in HBM (2 = contiguous (N,2,G,G) rewritten every step; default auto)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -70,7 +73,7 @@ def cpu_baseline(cfg, seconds: float):
                       f"OracleVecEnv, 1 process / 1 thread"}
 
 
-def load_traffic(workload: str, n_envs: int):
+def load_traffic(workload: str, n_envs: int, window: int):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if not os.path.exists(path):
@@ -78,7 +81,7 @@ def load_traffic(workload: str, n_envs: int):
     try:
         with open(path) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) != n_envs:
+        if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window:
             return None
         return float(d["raster_hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
@@ -119,7 +122,8 @@ def main():
         n = pr["n_envs"] // pr["gpus"]
         strong = False
     n_total = n * world
-    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline)
+    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
+                  frame_window=args.frame_window)
 
     K, W = args.steps, args.warmup
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -132,6 +136,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ep0 = int(env.episode.sum())
     t0 = time.perf_counter()
     for k in range(K):
         evs[k][0].record()
@@ -146,16 +151,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     env.check_errors()
+    resets = int(env.episode.sum()) - ep0  # auto-resets in the timed steps
 
-    # raster kernel: HIP events around every launch on the launch stream
-    r_ms = [a.elapsed_time(b) for a, b, _ in raster_ev]
-    r_envs = [m for _, _, m in raster_ev]
+    # raster kernel: HIP events around every launch on the launch stream; algorithmic bytes per
+    # launch from the frame-window schedule (full launches write both frames), plus the older
+    # frame of every env reset during a newest-only launch (resets spread evenly over launches)
+    r_ms = [r[0].elapsed_time(r[1]) for r in raster_ev]
+    n_full = sum(1 for r in raster_ev if r[4])
+    G2 = cfg.grid * cfg.grid
+    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * 4 * G2
     raster_ms = sum(r_ms) / len(r_ms)
     step_ms_ev = sum(a.elapsed_time(b) for a, b in evs) / K
-    b = bytes_per_env_step(cfg, potential=not args.no_potential)
-    achieved = b["raster"] * sum(r_envs) / (sum(r_ms) * 1e-3) / 1e9
-    per_launch_envs = r_envs[0]
-    traffic = load_traffic(name, per_launch_envs)
+    b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window)
+    achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
+    per_launch_envs = raster_ev[0][2]
+    traffic = load_traffic(name, per_launch_envs, env.frame_window)
 
     if rank == 0:
         out = {
@@ -174,14 +184,16 @@ def main():
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow),
+                       "frame_window": env.frame_window,
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
                          "kernel": "raster_kernel", "kernel_ms": raster_ms,
-                         "algorithmic_bytes_per_launch": b["raster"] * per_launch_envs,
-                         "launches_per_step": len(r_ms) // K},
+                         "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
+                         "launches_per_step": len(r_ms) // K, "full_launches": n_full,
+                         "timed_resets": resets},
             "raster_ms_per_step": sum(r_ms) / K,
             "step_ms_events": step_ms_ev,
             "pipeline_slices": env.pipeline_slices,

@@ -49,7 +49,7 @@ class StateT(C.Structure):
 class ObsT(C.Structure):
     _fields_ = [("state_m", C.c_void_p), ("state_g", C.c_void_p), ("state_v", C.c_void_p),
                 ("state_t", C.c_void_p), ("potential", C.c_void_p), ("grad", C.c_void_p), ("lidar", C.c_void_p),
-                ("flow", C.c_void_p)]
+                ("flow", C.c_void_p), ("state_m_stride", C.c_int64)]
 
 
 class OutT(C.Structure):
@@ -183,7 +183,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
 
 
 TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES = 1, 2, 3, 4
-RASTER_NT, RASTER_PLAIN, RASTER_XCD = 1, 2, 4
+RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
 
 
 def set_tuning(key: int, value: int) -> int:

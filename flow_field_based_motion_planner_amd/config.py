@@ -191,19 +191,21 @@ def preset(name: str, **overrides) -> FFMPConfig:
     return FFMPConfig(**kw)
 
 
-def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True) -> Dict[str, int]:
-    """Algorithmic HBM bytes of one env step (DESIGN.md §Roofline).
+def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True, window: int = 2) -> Dict[str, int]:
+    """Algorithmic HBM bytes of one env step (DESIGN.md §5).
 
-    raster kernel: writes both float32 frames of state_m (8 G^2), the float32
-    potential plane (4 G^2) and, with cfg.flow, the two float32 flow planes (8 G^2);
-    reads the raster record (64 + 48 K).  state kernel:
-    reads/writes pose, goal, d0, t, episode, obstacles and writes the small obs,
-    lidar and the record.
+    raster kernel: writes the new float32 frame of state_m (4 G^2), the older one too on the
+    steps where the frame window wraps (every W-1 steps; every step for W = 2) — plus, not
+    counted here, the older frame of each env reset on the other steps —, the float32 potential
+    plane (4 G^2) and, with cfg.flow, the two float32 flow planes (8 G^2); reads the raster
+    record (64 + 48 K).  state kernel: reads/writes pose, goal, d0, t, episode, obstacles and
+    writes the small obs, lidar and the record.
     """
     G2 = cfg.grid * cfg.grid
     K, L = cfg.n_obst, cfg.n_beams
     rec = 4 * cfg.record_len()
-    raster = 8 * G2 + (4 * G2 if potential else 0) + (8 * G2 if cfg.flow else 0) + rec
+    frames = 4 * G2 + (4 * G2) // (max(int(window), 2) - 1)
+    raster = frames + (4 * G2 if potential else 0) + (8 * G2 if cfg.flow else 0) + rec
     state_rw = 2 * (24 + 16 + 8 + 4 + 4 + 40 * K)  # pose, goal, d0, t, episode, obst(32)+r(8)
     small_obs = 4 * (2 + 2 + 1 + 2) + 4 * L + rec + 8 + 4 + 4  # g, v, t, grad, lidar, record, action, reward, flags
     return {"raster": raster, "state": state_rw + small_obs, "total": raster + state_rw + small_obs}

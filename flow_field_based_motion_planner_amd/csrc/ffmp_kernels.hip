@@ -114,11 +114,11 @@ FFMP_DEV void wave_sync() {
 // One env's raster record: header, goal, then K float4 of each of cur / prev / vel.
 // Lane k writes obstacle k; lanes 0..3 the header words.
 FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const FrameHdr& hc, const FrameHdr& hp,
-                           float2 ge, float4 ecur, float4 eprev, float4 vel) {
+                           float2 ge, float4 ecur, float4 eprev, float4 vel, float first) {
   if (lane == 0) {
     rec[8] = ge.x;
     rec[9] = ge.y;
-    rec[10] = 0.0f;
+    rec[10] = first;  // 1: written by a reset, the two frames are identical
     rec[11] = 0.0f;
   }
   if (lane < 4) {
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
     }
     if (reset_now && st.term_record)  // the terminal state, before the reset below overwrites it
       write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev,
-                   to_ego(gx, gy, x1, y1, c1, s1), s_ecur[lane], s_eprev[lane], ego_vel(my, c1, s1));
+                   to_ego(gx, gy, x1, y1, c1, s1), s_ecur[lane], s_eprev[lane], ego_vel(my, c1, s1), 0.0f);
   }
 
   if (reset_now) {
@@ -315,9 +315,10 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
     const float4 ecur = has_obst ? s_ecur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 eprev = has_obst ? s_eprev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 vel = ego_vel(my, c1, s1);
-    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel);
+    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel,
+                 reset_now ? 1.0f : 0.0f);
     if (MODE == kEnvMode_Step && !reset_now && st.term_record)
-      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel);
+      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
   }
 
   // ---- write back state / obs / outputs ----
@@ -390,7 +391,8 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
                                                      const uint8_t* __restrict__ mask,
-                                                     float* __restrict__ state_m,
+                                                     float* __restrict__ state_m, int64_t sm_stride,
+                                                     int32_t newest_only,
                                                      float* __restrict__ pot,
                                                      float* __restrict__ flow) {
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
@@ -430,6 +432,9 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const FrameHdr hc{s_hdr[0], s_hdr[1], s_hdr[2], s_hdr[3]};
   const FrameHdr hp{s_hdr[4], s_hdr[5], s_hdr[6], s_hdr[7]};
   const float gx = s_hdr[8], gy = s_hdr[9];
+  // temporal stack in place: the older frame already holds the previous newest one unless this
+  // env was reset (block-uniform)
+  const bool write_old = !newest_only || s_hdr[10] != 0.0f;
   const float res = cfg.res_f, half = cfg.half_f;
   const float invG = 1.0f / (float)G;
 
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   // lanes 0..3: corners of the current frame, 4..7: previous frame
   const FrameHdr hq = (lane < 4) ? hc : hp;
 
-  float* m0 = state_m + (int64_t)e * 2 * G2;
+  float* m0 = state_m + e * sm_stride;
   float* m1 = m0 + G2;
   float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
   float* f0 = FLOW ? flow + (int64_t)e * 2 * G2 : nullptr;
@@ -465,11 +470,11 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
 
     // ---- lane-parallel cull ----
     const uint64_t mc = __ballot(has && box_dist2(oc.x, oc.y, bx0, bx1, by0, by1) <= rc2);
-    const uint64_t mp = __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2);
+    const uint64_t mp = write_old ? __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2) : 0ull;
     const uint64_t wb = __ballot(lane >= 8 || corner_inside(cfg, hq, (lane & 1) ? bx1 : bx0,
                                                              (lane & 2) ? by1 : by0));
     const bool walls_c = (wb & 0xFull) != 0xFull;
-    const bool walls_p = (wb & 0xF0ull) != 0xF0ull;
+    const bool walls_p = write_old && (wb & 0xF0ull) != 0xF0ull;
 
     // ---- this lane's 4 cells ----
     const int off = r0 + lane * 4;
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
         U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
       }
     }
-    store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
+    if (write_old) store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
     store4<NT>(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
     if (pp) store4<NT>(pp + q, U[0], U[1], U[2], U[3]);
     if (FLOW) {
@@ -843,11 +848,15 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
   const bool fl = cfg->flow != 0;
   if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
+  const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
+  if (sm_stride < 2 * (int64_t)G2)
+    return fail(FFMP_E_ARG, "state_m_stride %lld < 2*G*G", (long long)obs->state_m_stride);
+  const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
   const dim3 grid((unsigned)blocks), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define FFMP_RASTER_LAUNCH(NT_, XCD_, FL_)                                                              \
   hipLaunchKernelGGL((raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, \
-                     obs->state_m, obs->potential, obs->flow)
+                     obs->state_m, sm_stride, newest, obs->potential, obs->flow)
   const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
   switch (sel) {
     case 0: FFMP_RASTER_LAUNCH(false, false, false); break;

@@ -48,12 +48,20 @@ class FFMPVec:
         keep_terminal: also keep every env's post-step state before auto-reset
             (`term_record` (N, record_len) and `term_obs` (N, 5) = state_g, state_v, state_t):
             what a transition store needs for envs that just finished (ReplayMemory).
+        frame_window: W >= 2 frames per env kept in HBM (`frames` (N, W, G, G)); `state_m` is
+            the view frames[:, p:p+2] of the current [older, newest] pair.  Each step slides
+            the pair by one frame and writes only the new frame (plus the older one of envs
+            that reset): the temporal stack of make_temporal_maps (train.py:474-486) kept in
+            place instead of re-written.  Every W-1 steps the pair wraps to slot 0 (both frames
+            written).  W = 2 is the contiguous (N,2,G,G) layout.  None: 8 for large batches
+            when HBM allows, else 2.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
-                 autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False):
+                 autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
+                 frame_window: Optional[int] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -76,11 +84,15 @@ class FFMPVec:
         self.keep_terminal = bool(keep_terminal)
         self.placement = None
         self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
+        self.frame_window = self._pick_window(frame_window)
+        self._wpos = 0  # frame slot of state_m[:, 0]
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
         if pipeline is None:
             pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt)
         self.pipeline_slices = max(1, min(int(pipeline), self.num_envs))
+        if self.pipeline_slices > 1 and self.frame_window != 2:
+            raise ValueError("pipeline > 1 needs frame_window=2")
         self._build_structs()
         plane_bytes = self._nbytes((self.num_envs, (3 if potential else 2) + (2 if self.cfg.flow else 0), G2),
                                    torch.float32)
@@ -92,6 +104,22 @@ class FFMPVec:
 
     # ------------------------------------------------------------------ setup
     _ARENA_ALIGN = 2 << 20
+    WINDOW_DEFAULT = 8
+    WINDOW_HBM_FRACTION = 0.6  # auto window: frames + other planes within this share of free HBM
+
+    def _pick_window(self, w: Optional[int]) -> int:
+        if w is not None:
+            if int(w) < 2:
+                raise ValueError("frame_window must be >= 2")
+            return int(w)
+        cfg, N = self.cfg, self.num_envs
+        plane = N * cfg.grid * cfg.grid * 4
+        if plane * 3 < self.AUTOTUNE_MIN_BYTES:
+            return 2
+        other = plane * ((1 if self.with_potential else 0) + (2 if cfg.flow else 0))
+        free, _ = torch.cuda.mem_get_info(self.device)
+        budget = self.WINDOW_HBM_FRACTION * free - other
+        return int(max(2, min(self.WINDOW_DEFAULT, budget // plane)))
 
     def _buffer_specs(self):
         """(name, shape, dtype) of every per-shard device buffer."""
@@ -100,7 +128,7 @@ class FFMPVec:
         f32, f64, i32, b = torch.float32, torch.float64, torch.int32, torch.bool
         specs = [
             # observation planes first: the big, hot, write-streamed buffers
-            ("state_m", (N, 2, G, G), f32),
+            ("frames", (N, self.frame_window, G, G), f32),
             ("potential", (N, G, G), f32),
             ("flow", (N, 2, G, G), f32),
             # state
@@ -193,8 +221,8 @@ class FFMPVec:
         for _ in range(steps):
             self.step(a, timing=t)
         torch.cuda.synchronize(self.device)
-        ms = sum(x.elapsed_time(y) for x, y, _ in t) / len(t)
-        b = bytes_per_env_step(self.cfg, potential=self.with_potential)["raster"] * self.num_envs
+        ms = sum(x.elapsed_time(y) for x, y, *_ in t)
+        b = sum(r[3] for r in t)
         return b / (ms * 1e-3) / 1e9
 
     # Placement retries.  Even the best shape runs ~15 % slower on a "slow" placement (e.g.
@@ -242,6 +270,8 @@ class FFMPVec:
         results = []
         plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) + (1.0 if self.flow is not None else 0.0))
         steps = 3 if plane_bytes >= (8 << 30) else 12  # >= ~10 ms of timed raster per shape
+        cyc = self.frame_window - 1  # whole window cycles: one full raster + W-2 newest-only
+        steps = -(-steps // cyc) * cyc
         for shape in self.RASTER_SHAPES:
             self.raster_shape = shape
             results.append((self._raster_gbs_steady(steps), shape))
@@ -259,9 +289,10 @@ class FFMPVec:
                                     self.obst.data_ptr(), self.obst_r.data_ptr(), self.t.data_ptr(),
                                     self.episode.data_ptr(), self.record.data_ptr(), self.err.data_ptr(),
                                     _ptr(self.term_record), _ptr(self.term_obs))
+        G2 = self.cfg.grid * self.cfg.grid
         self._obs_c = _abi.ObsT(self.state_m.data_ptr(), self.state_g.data_ptr(), self.state_v.data_ptr(),
                                 self.state_t.data_ptr(), _ptr(self.potential), self.grad.data_ptr(),
-                                _ptr(self.lidar), _ptr(self.flow))
+                                _ptr(self.lidar), _ptr(self.flow), self.frame_window * G2)
         self._out_c = _abi.OutT(self.reward.data_ptr(), self.done.data_ptr(), self.is_goal.data_ptr(),
                                 self.collision.data_ptr(), self.truncated.data_ptr())
         self._build_slices()
@@ -298,6 +329,36 @@ class FFMPVec:
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    # ------------------------------------------------------------ frame window
+    @property
+    def state_m(self) -> torch.Tensor:
+        """(N, 2, G, G) [older, newest] view of the frame window (contiguous iff W == 2)."""
+        return self.frames[:, self._wpos:self._wpos + 2]
+
+    def _set_window(self, p: int) -> None:
+        self._wpos = p
+        self._obs_c.state_m = self.frames.data_ptr() + p * self.cfg.grid * self.cfg.grid * 4
+
+    def _raster_bytes(self, n: int, full: bool) -> int:
+        """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs
+        reset during a newest-only launch: 4 G^2 each, added by bench.py from the episode counts)."""
+        G2 = self.cfg.grid * self.cfg.grid
+        per = (8 if full else 4) * G2 + (4 * G2 if self.potential is not None else 0) + \
+            (8 * G2 if self.flow is not None else 0) + 4 * self.cfg.record_len()
+        return n * per
+
+    def _raster_launch(self, full: bool, mask=None, timing: Optional[list] = None) -> None:
+        flags = self.raster_shape[1] | (0 if full else _abi.RASTER_NEWEST)
+        if timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(mask),
+                                           C.byref(self._obs_c), self.raster_shape[0], flags, self._stream()),
+                   "ffmp_raster")
+        if timing is not None:
+            e1.record()
+            timing.append((e0, e1, self.num_envs, self._raster_bytes(self.num_envs, full), full))
+
     # --------------------------------------------------------------- gym API
     @property
     def obs(self) -> Dict[str, torch.Tensor]:
@@ -328,10 +389,11 @@ class FFMPVec:
                     raise ValueError("mask must have num_envs elements")
             initial = 1 if (mask is None) else 0
             s = self._stream()
+            if mask is None:
+                self._set_window(0)
             _abi.check(self.lib.ffmp_reset(C.byref(self._cfg_c), self.num_envs, self.env_offset, _ptr(m), initial,
                                            C.byref(self._state_c), C.byref(self._obs_c), s), "ffmp_reset")
-            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
-                                               C.byref(self._obs_c), *self.raster_shape, s), "ffmp_raster")
+            self._raster_launch(True, m)
             self._mask_keepalive = m
         self._needs_reset = False
         return self._obs_out(copy)
@@ -354,10 +416,17 @@ class FFMPVec:
                                             self._stream()), "ffmp_step_state")
 
     def raster(self, mask: Optional[torch.Tensor] = None) -> None:
-        """Kernel 2 of a step: state_m frames and potential plane (the HBM-bound hot kernel)."""
+        """Re-raster the current observation (both frames, potential, flow) from the record."""
         m = None if mask is None else mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
-        _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(m),
-                                           C.byref(self._obs_c), *self.raster_shape, self._stream()), "ffmp_raster")
+        self._raster_launch(True, m)
+
+    def raster_step(self, timing: Optional[list] = None) -> None:
+        """Kernel 2 of a step (the HBM-bound hot kernel): slide the frame pair by one and raster
+        the new frame + potential (+ flow), or both frames when the window wraps or W == 2."""
+        p = self._wpos + 1
+        full = p > self.frame_window - 2
+        self._set_window(0 if full else p)
+        self._raster_launch(full, None, timing)
 
     def _step_pipelined(self, actions, timing) -> None:
         a = self._actions(actions)
@@ -382,14 +451,14 @@ class FFMPVec:
                        "ffmp_raster")
             if timing is not None:
                 e1.record(main)
-                timing.append((e0, e1, n))
+                timing.append((e0, e1, n, self._raster_bytes(n, True), True))
 
     def step(self, actions, copy: bool = False, timing: Optional[list] = None
              ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor, dict]:
         """Advance every env one step. Returns (obs, reward f32[N], done bool[N], info).
 
-        `timing`: optional list; (start, end, n_envs) HIP-event pairs around each raster launch
-        (on the caller's stream) are appended to it."""
+        `timing`: optional list; (start, end, n_envs, algorithmic bytes, full) per raster launch
+        (HIP events on the caller's stream) are appended to it."""
         if self._needs_reset:
             raise RuntimeError("call reset() before step()")
         with torch.cuda.device(self.device):
@@ -397,13 +466,7 @@ class FFMPVec:
                 self._step_pipelined(actions, timing)
             else:
                 self.step_state(actions)
-                if timing is not None:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                self.raster()
-                if timing is not None:
-                    e1.record()
-                    timing.append((e0, e1, self.num_envs))
+                self.raster_step(timing)
         info = {"is_goal": self.is_goal, "collision": self.collision, "truncated": self.truncated,
                 "step": self.t, "episode": self.episode}
         if copy:
@@ -444,7 +507,8 @@ class FFMPVec:
     def __repr__(self):
         c = self.cfg
         return (f"FFMPVec(num_envs={self.num_envs}, G={c.grid}, K={c.n_obst}, L={c.n_beams}, "
-                f"moving={c.moving}, device={self.device}, env_offset={self.env_offset})")
+                f"moving={c.moving}, device={self.device}, env_offset={self.env_offset}, "
+                f"frame_window={self.frame_window})")
 
 
 __all__ = ["FFMPVec", "PRESETS"]

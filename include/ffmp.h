@@ -131,6 +131,9 @@ typedef struct ffmp_obs {
   float* lidar;     /* (N,L) ranges (+inf = no return, -inf = inside), NULL if L == 0 */
   float* flow;      /* (N,2,G,G) ego-frame velocity (m/s) of the disc covering each cell of the
                        newest frame (lowest disc index wins), 0 elsewhere; NULL unless cfg.flow */
+  int64_t state_m_stride; /* floats from env e's [older, newest] pair to env e+1's; 0 = 2*G*G
+                             (contiguous).  A frame window (N, W, G, G) is viewed with stride W*G*G
+                             and state_m pointing at the older slot (see FFMP_RASTER_NEWEST). */
 } ffmp_obs_t;
 
 /* Per-step outputs (device pointers, N each). Flags are 0/1 bytes. */
@@ -181,7 +184,8 @@ int ffmp_step_state(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
                     ffmp_out_t* out, void* stream);
 
 /* Raster state_m[:,0] (previous frame), state_m[:,1] (current frame) and the
- * potential plane from the raster record (mask NULL = all envs). */
+ * potential plane from the raster record (mask NULL = all envs).  Record word 10 is 1 for a
+ * record written by a reset (its two frames are identical), else 0. */
 int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                 const uint8_t* mask, ffmp_obs_t* obs, void* stream);
 
@@ -191,6 +195,12 @@ int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
 #define FFMP_RASTER_NT 1     /* nontemporal 16-B stores          */
 #define FFMP_RASTER_PLAIN 2  /* plain 16-B stores                */
 #define FFMP_RASTER_XCD 4    /* XCD-aware block -> (env, tile) remap */
+#define FFMP_RASTER_NEWEST 8 /* temporal stack in place (make_temporal_maps keeps the previous frame,
+                                train.py:474-486): write state_m[:,1] (+ potential / flow) for every
+                                env but state_m[:,0] only for envs whose record is a first frame
+                                (reset: older == newest); the caller points state_m one frame past
+                                the previous call's older slot, so [:,0] already holds the previous
+                                newest frame */
 int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                    const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
                    int32_t flags, void* stream);

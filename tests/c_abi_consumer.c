@@ -1,6 +1,7 @@
 /* c_abi_consumer.c — a plain-C consumer of libffmp (include/ffmp.h): no Python, no torch.
- * Allocates every buffer with hipMalloc, fills the config by hand, resets and steps N envs,
- * and checks size-independent invariants:
+ * Allocates every buffer with hipMalloc, fills the config by hand, resets and steps N envs with
+ * the temporal stack kept in place (a frame window of W frames per env, FFMP_RASTER_NEWEST), and
+ * checks size-independent invariants:
  *   - every state_m cell is 0 or 255,
  *   - the older frame equals the previous newest frame for envs that did not reset,
  *   - a reset env's two frames are identical,
@@ -43,7 +44,7 @@ static void* dalloc(size_t bytes) {
 
 int main(void) {
   const int64_t N = 512;
-  const int G = 128, K = 12, L = 90, STEPS = 25;
+  const int G = 128, K = 12, L = 90, STEPS = 25, W = 4;
   if (ffmp_abi_version() != FFMP_ABI_VERSION) {
     fprintf(stderr, "ABI mismatch\n");
     return 4;
@@ -78,9 +79,10 @@ int main(void) {
                      (double*)dalloc(N * K * 4 * 8), (double*)dalloc(N * K * 8), (int32_t*)dalloc(N * 4),
                      (int32_t*)dalloc(N * 4), (float*)dalloc(N * rec * 4), (uint32_t*)dalloc(4),
                      NULL, NULL /* no terminal record / obs */};
-  ffmp_obs_t ob = {(float*)dalloc(N * 2 * G2 * 4), (float*)dalloc(N * 2 * 4), (float*)dalloc(N * 2 * 4),
+  float* frames = (float*)dalloc(N * W * G2 * 4); /* (N, W, G, G); state_m = slots [p, p+1] */
+  ffmp_obs_t ob = {frames, (float*)dalloc(N * 2 * 4), (float*)dalloc(N * 2 * 4),
                    (float*)dalloc(N * 4), (float*)dalloc(N * G2 * 4), (float*)dalloc(N * 2 * 4),
-                   (float*)dalloc(N * L * 4), NULL};
+                   (float*)dalloc(N * L * 4), NULL, (int64_t)W * (int64_t)G2};
   ffmp_out_t out = {(float*)dalloc(N * 4), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N),
                     (uint8_t*)dalloc(N)};
   int64_t* act = (int64_t*)dalloc(N * 8);
@@ -90,8 +92,9 @@ int main(void) {
 
   hipStream_t s;
   HIPCHK(hipStreamCreate(&s));
+  int p = 0; /* frame slot of state_m[:, 0] */
   FFCHK(ffmp_reset(&cfg, N, 0, NULL, 1, &st, &ob, s));
-  FFCHK(ffmp_raster(&cfg, N, st.record, NULL, &ob, s));
+  FFCHK(ffmp_raster_ex(&cfg, N, st.record, NULL, &ob, 0, 0, s));
 
   float* sm = (float*)malloc(N * 2 * G2 * 4);
   float* prev_new = (float*)malloc(N * G2 * 4);
@@ -101,7 +104,10 @@ int main(void) {
   float* mr = (float*)malloc(N * 4);
   int64_t* act_h = (int64_t*)malloc(N * 8);
   HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipMemcpy(sm, ob.state_m, N * 2 * G2 * 4, hipMemcpyDeviceToHost));
+  /* the [older, newest] pairs of all envs: N rows of 2*G2 floats, W*G2 floats apart */
+#define COPY_PAIRS() \
+  HIPCHK(hipMemcpy2D(sm, 2 * G2 * 4, ob.state_m, (size_t)W * G2 * 4, 2 * G2 * 4, N, hipMemcpyDeviceToHost))
+  COPY_PAIRS();
   for (int64_t e = 0; e < N; ++e) memcpy(prev_new + e * G2, sm + (e * 2 + 1) * G2, G2 * 4);
 
   uint64_t rng = 88172645463325252ull;
@@ -113,9 +119,16 @@ int main(void) {
       act_h[e] = (int64_t)(rng % FFMP_N_ACTIONS);
     }
     HIPCHK(hipMemcpyAsync(act, act_h, N * 8, hipMemcpyHostToDevice, s));
-    FFCHK(ffmp_step(&cfg, N, 0, act, &st, &ob, &out, s));
+    FFCHK(ffmp_step_state(&cfg, N, 0, act, &st, &ob, &out, s));
+    /* slide the pair one frame; the older slot already holds the previous newest frame, so
+     * only the new one is written (and the older one of envs that reset) — until the window
+     * wraps, when both frames are written at slot 0 */
+    int32_t flags = FFMP_RASTER_NEWEST;
+    if (++p > W - 2) { p = 0; flags = 0; }
+    ob.state_m = frames + (size_t)p * G2;
+    FFCHK(ffmp_raster_ex(&cfg, N, st.record, NULL, &ob, 0, flags, s));
     HIPCHK(hipStreamSynchronize(s));
-    HIPCHK(hipMemcpy(sm, ob.state_m, N * 2 * G2 * 4, hipMemcpyDeviceToHost));
+    COPY_PAIRS();
     HIPCHK(hipMemcpy(pot, ob.potential, N * G2 * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(grad, ob.grad, N * 2 * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(done, out.done, N, hipMemcpyDeviceToHost));

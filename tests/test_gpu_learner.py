@@ -64,7 +64,7 @@ def test_replay_update_matches_reference_formulas():
     for (k, p), (_, q) in zip(brain.main_q_network.named_parameters(), main0.named_parameters()):
         gmax = float(q.grad.abs().max())
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-3, atol=1e-4 * gmax + 1e-12, msg=k)
-        d = (p - q).abs()
+        d = (p - q).detach().abs()
         assert float(d.max()) <= 2 * 0.0005 + 1e-6, k
         assert float((d <= 1e-6).float().mean()) > 0.9, k
     brain.update_target_q_network()

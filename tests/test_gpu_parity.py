@@ -30,8 +30,9 @@ CASES = {
 }
 
 
-def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True):
-    env = FFMPVec(n, cfg, device="cuda:0", env_offset=env_offset, keep_terminal=keep_terminal)
+def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True, frame_window=None):
+    env = FFMPVec(n, cfg, device="cuda:0", env_offset=env_offset, keep_terminal=keep_terminal,
+                  frame_window=frame_window)
     ref = OracleVecEnv(cfg, n, env_offset=env_offset)
     env.reset()
     ref.reset()
@@ -56,7 +57,10 @@ def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True):
 @pytest.mark.parametrize("name", list(CASES))
 def test_step_parity(name):
     cfg, n, steps = CASES[name]
-    env, ref, problems, counts = _run(cfg, n, steps, keep_terminal=name != "C2_128_static")
+    # half the cases keep the temporal stack in a 4-frame window (pair slides, wraps every 3 steps)
+    window = 4 if name in ("C1_64_static", "dense_collisions", "flow_planes", "C3_256_moving_lidar") else 2
+    env, ref, problems, counts = _run(cfg, n, steps, keep_terminal=name != "C2_128_static", frame_window=window)
+    assert env.frame_window == window
     assert not problems, "\n".join(problems[:20])
     if name == "dense_collisions":
         assert counts["collision"] > 0 and counts["done"] > 0, counts  # the reset path is exercised
@@ -239,3 +243,40 @@ def test_autotune_picks_a_candidate():
         env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))  # autotune leaves it un-reset
     env.reset()
     env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))
+
+
+@pytest.mark.parametrize("window", [3, 4, 8])
+def test_frame_window_equals_contiguous(window):
+    """The in-place temporal stack (frame window W, newest-only rasters + wraps) yields the same
+    observations, bit for bit, as rewriting both frames every step (W = 2), across resets."""
+    cfg = FFMPConfig(grid=64, n_obst=24, n_beams=16, moving=True, obst_rmax=0.6, obst_vmax=1.5, world_half=3.0,
+                     max_steps=7, flow=True, seed=41)
+    n = 40
+    a = FFMPVec(n, cfg, device="cuda:0", frame_window=2)
+    b = FFMPVec(n, cfg, device="cuda:0", frame_window=window)
+    assert not b.state_m.is_contiguous() and b.state_m.shape == a.state_m.shape
+    a.reset()
+    b.reset()
+    assert torch.equal(a.state_m, b.state_m)
+    rng = np.random.default_rng(window)
+    resets = 0
+    for s in range(3 * window + 5):
+        act = torch.as_tensor(rng.integers(0, 28, n), device="cuda:0")
+        oa, _, da, _ = a.step(act)
+        ob, _, db, _ = b.step(act)
+        resets += int(da.sum())
+        assert torch.equal(oa["state_m"], ob["state_m"]), s
+        assert torch.equal(oa["potential"], ob["potential"]) and torch.equal(oa["flow"], ob["flow"])
+        assert torch.equal(da, db)
+        if s == window:  # masked reset mid-window
+            m = torch.zeros(n, dtype=torch.bool, device="cuda:0")
+            m[::5] = True
+            a.reset(mask=m)
+            b.reset(mask=m)
+            assert torch.equal(a.state_m, b.state_m)
+    assert resets > 0
+    sd = b.state_dict()  # checkpoint round trip re-rasters the current pair in place
+    b.state_m.fill_(-1.0)
+    b.load_state_dict(sd)
+    assert torch.equal(a.state_m, b.state_m)
+

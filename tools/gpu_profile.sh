@@ -10,11 +10,13 @@ CFG=${2:-C3}
 mkdir -p $R/gpurun_out/prof
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.build()" || exit 1
-BENCH="$R/bench.py --config $CFG --steps 50 --warmup 10 --cpu-seconds 0"
+# 49 timed steps = 7 whole frame-window cycles (W = 8), so trace and PMC passes average the same
+# mix of full and newest-only raster launches
+BENCH="$R/bench.py --config $CFG --steps 49 --warmup 10 --cpu-seconds 0"
 echo "== trace"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/trace_$CFG -o run -- python3 $BENCH > $R/gpurun_out/prof/bench_trace_$CFG.log 2>&1 || exit 1
 echo "== pmc write"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 8 --warmup 2 --cpu-seconds 0 > $R/gpurun_out/prof/bench_pmcw_$CFG.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 > $R/gpurun_out/prof/bench_pmcw_$CFG.log 2>&1 || exit 1
 echo "== pmc fetch"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 8 --warmup 2 --cpu-seconds 0 > $R/gpurun_out/prof/bench_pmcf_$CFG.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 > $R/gpurun_out/prof/bench_pmcf_$CFG.log 2>&1 || exit 1
 cd $R && python3 tools/summarize_profiles.py $TAG $CFG

@@ -43,5 +43,5 @@ for shape in [(4096, 2), (2048, 2), (2048, 6), (2048, 1)]:
     for k in range(5, 25):
         env.step(acts[k], timing=t)
     torch.cuda.synchronize()
-    c = b / (sum(x.elapsed_time(y) for x, y, _ in t) / len(t)) / 1e6
+    c = b / (sum(x.elapsed_time(y) for x, y, *_ in t) / len(t)) / 1e6
     print(f"{name} shape {shape}: A {a:.0f}  B {bb:.0f}  C {c:.0f}", flush=True)

@@ -5,7 +5,10 @@
   profiles/<tag>_<cfg>_bench.json         the bench.py JSON line printed under that trace
   profiles/<tag>_<cfg>_pmc.json           per-kernel WRITE_SIZE / FETCH_SIZE (separate --pmc passes),
                                           converted to bytes per launch with the gfx950 correction
-                                          (FETCH_SIZE counts half of wide streaming reads: x2)
+                                          (FETCH_SIZE counts half of wide streaming reads: x2);
+                                          raster: mean over the pass's timed launches (the frame
+                                          window mixes full and newest-only launches), other
+                                          kernels: median over dispatches
   profiles/pmc_traffic_<cfg>.json         what bench.py reads for roofline.traffic
 """
 import csv
@@ -34,15 +37,28 @@ def bench_json(log):
 
 
 def counters(path, name):
+    """kernel -> counter values in dispatch order."""
     per = {}
     with open(path) as f:
-        for row in csv.DictReader(f):
-            if row.get("Counter_Name") != name:
-                continue
-            k = row["Kernel_Name"]
-            key = "raster_kernel" if "raster_kernel" in k else ("env_kernel" if "env_kernel" in k else k)
-            per.setdefault(key, []).append(float(row["Counter_Value"]))
+        rows = sorted((r for r in csv.DictReader(f) if r.get("Counter_Name") == name),
+                      key=lambda r: int(r["Dispatch_Id"]))
+    for row in rows:
+        k = row["Kernel_Name"]
+        key = "raster_kernel" if "raster_kernel" in k else ("env_kernel" if "env_kernel" in k else k)
+        per.setdefault(key, []).append(float(row["Counter_Value"]))
     return per
+
+
+def timed_launches(log):
+    bj = bench_json(log) if os.path.exists(log) else None
+    return bj["steps"] * bj["roofline"].get("launches_per_step", 1) if bj else None
+
+
+def per_launch(vals, key, k):
+    if key == "raster_kernel" and k:
+        tail = vals[-k:]
+        return sum(tail) / len(tail)
+    return statistics.median(vals)
 
 
 def main():
@@ -58,25 +74,28 @@ def main():
             json.dump(bj, f, indent=1)
     w = counters(find(f"pmcw_{cfg}/**/run_counter_collection.csv"), "WRITE_SIZE")
     r = counters(find(f"pmcf_{cfg}/**/run_counter_collection.csv"), "FETCH_SIZE")
-    pm = {"workload": cfg, "units": "bytes per launch (median over dispatches)",
+    kw = timed_launches(os.path.join(PROF, f"bench_pmcw_{cfg}.log"))
+    kf = timed_launches(os.path.join(PROF, f"bench_pmcf_{cfg}.log"))
+    pm = {"workload": cfg, "units": "bytes per launch (raster: mean over the timed launches; others: median)",
           "correction": "WRITE_SIZE*1024 exact for 16-B/lane streaming stores; FETCH_SIZE*1024*2 (gfx950 halves wide "
                         "streaming reads, MI355X_MICROARCH.md HBM section)", "kernels": {}}
     for k in sorted(set(w) | set(r)):
-        wb = statistics.median(w.get(k, [0.0])) * 1024
-        fb = statistics.median(r.get(k, [0.0])) * 1024 * 2
+        wb = per_launch(w.get(k, [0.0]), k, kw) * 1024
+        fb = per_launch(r.get(k, [0.0]), k, kf) * 1024 * 2
         pm["kernels"][k] = {"write_bytes": wb, "fetch_bytes_corrected": fb, "hbm_bytes": wb + fb,
                             "dispatches": len(w.get(k, []))}
     if bj:
         n = bj["config"]["n_envs_per_gpu"]
         alg = bj["roofline"]["algorithmic_bytes_per_launch"]
         pm["n_envs"] = n
+        pm["frame_window"] = bj["config"].get("frame_window", 2)
         pm["raster_algorithmic_bytes_per_launch"] = alg
         if "raster_kernel" in pm["kernels"]:
             hb = pm["kernels"]["raster_kernel"]["hbm_bytes"]
             pm["raster_traffic_over_algorithmic"] = hb / alg
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
-                json.dump({"n_envs": n, "raster_hbm_bytes_per_launch": hb, "source": f"{tag}_{cfg}_pmc.json"}, f,
-                          indent=1)
+                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "raster_hbm_bytes_per_launch": hb,
+                           "source": f"{tag}_{cfg}_pmc.json"}, f, indent=1)
     trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")
     if trace and bj:
         # the last (steps x launches_per_step) raster dispatches are exactly the launches bench.py

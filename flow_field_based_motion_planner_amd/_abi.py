@@ -49,7 +49,7 @@ class StateT(C.Structure):
 class ObsT(C.Structure):
     _fields_ = [("state_m", C.c_void_p), ("state_g", C.c_void_p), ("state_v", C.c_void_p),
                 ("state_t", C.c_void_p), ("potential", C.c_void_p), ("grad", C.c_void_p), ("lidar", C.c_void_p),
-                ("flow", C.c_void_p), ("state_m_stride", C.c_int64)]
+                ("flow", C.c_void_p), ("state_m_stride", C.c_int64), ("state_m_frame_stride", C.c_int64)]
 
 
 class OutT(C.Structure):

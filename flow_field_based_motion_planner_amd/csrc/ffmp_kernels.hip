@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
                                                      const float* __restrict__ record,
                                                      const uint8_t* __restrict__ mask,
                                                      float* __restrict__ state_m, int64_t sm_stride,
-                                                     int32_t newest_only,
+                                                     int64_t sm_frame, int32_t newest_only,
                                                      float* __restrict__ pot,
                                                      float* __restrict__ flow) {
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const FrameHdr hq = (lane < 4) ? hc : hp;
 
   float* m0 = state_m + e * sm_stride;
-  float* m1 = m0 + G2;
+  float* m1 = m0 + sm_frame;
   float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
   float* f0 = FLOW ? flow + (int64_t)e * 2 * G2 : nullptr;
 
@@ -849,14 +849,16 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   const bool fl = cfg->flow != 0;
   if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
   const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
-  if (sm_stride < 2 * (int64_t)G2)
-    return fail(FFMP_E_ARG, "state_m_stride %lld < 2*G*G", (long long)obs->state_m_stride);
+  const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
+  if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
+    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld floats (G*G = %d)",
+                (long long)sm_stride, (long long)sm_frame, G2);
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
   const dim3 grid((unsigned)blocks), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define FFMP_RASTER_LAUNCH(NT_, XCD_, FL_)                                                              \
   hipLaunchKernelGGL((raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, \
-                     obs->state_m, sm_stride, newest, obs->potential, obs->flow)
+                     obs->state_m, sm_stride, sm_frame, newest, obs->potential, obs->flow)
   const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
   switch (sel) {
     case 0: FFMP_RASTER_LAUNCH(false, false, false); break;

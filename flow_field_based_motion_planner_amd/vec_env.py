@@ -48,13 +48,14 @@ class FFMPVec:
         keep_terminal: also keep every env's post-step state before auto-reset
             (`term_record` (N, record_len) and `term_obs` (N, 5) = state_g, state_v, state_t):
             what a transition store needs for envs that just finished (ReplayMemory).
-        frame_window: W >= 2 frames per env kept in HBM (`frames` (N, W, G, G)); `state_m` is
-            the view frames[:, p:p+2] of the current [older, newest] pair.  Each step slides
-            the pair by one frame and writes only the new frame (plus the older one of envs
-            that reset): the temporal stack of make_temporal_maps (train.py:474-486) kept in
-            place instead of re-written.  Every W-1 steps the pair wraps to slot 0 (both frames
-            written).  W = 2 is the contiguous (N,2,G,G) layout.  None: 8 for large batches
-            when HBM allows, else 2.
+        frame_window: W >= 2 frames per env kept in HBM.  W > 2: a slot-major ring `frames`
+            (W, N, G, G) and `state_m` = the (N,2,G,G) view frames[p:p+2].transpose(0, 1) of the
+            current [older, newest] pair.  Each step slides the pair by one slot and writes only
+            the new frame (plus the older one of envs that reset): the temporal stack of
+            make_temporal_maps (train.py:474-486) kept in place instead of re-written, as one
+            contiguous plane per slot.  Every W-1 steps the pair wraps to slot 0 (both frames
+            written).  W = 2: the contiguous (N,2,G,G) layout, both frames written every step.
+            None: 8 for large batches when HBM allows, else 2.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -128,7 +129,7 @@ class FFMPVec:
         f32, f64, i32, b = torch.float32, torch.float64, torch.int32, torch.bool
         specs = [
             # observation planes first: the big, hot, write-streamed buffers
-            ("frames", (N, self.frame_window, G, G), f32),
+            ("frames", (N, 2, G, G) if self.frame_window == 2 else (self.frame_window, N, G, G), f32),
             ("potential", (N, G, G), f32),
             ("flow", (N, 2, G, G), f32),
             # state
@@ -292,7 +293,7 @@ class FFMPVec:
         G2 = self.cfg.grid * self.cfg.grid
         self._obs_c = _abi.ObsT(self.state_m.data_ptr(), self.state_g.data_ptr(), self.state_v.data_ptr(),
                                 self.state_t.data_ptr(), _ptr(self.potential), self.grad.data_ptr(),
-                                _ptr(self.lidar), _ptr(self.flow), self.frame_window * G2)
+                                _ptr(self.lidar), _ptr(self.flow), *self._sm_strides())
         self._out_c = _abi.OutT(self.reward.data_ptr(), self.done.data_ptr(), self.is_goal.data_ptr(),
                                 self.collision.data_ptr(), self.truncated.data_ptr())
         self._build_slices()
@@ -333,11 +334,19 @@ class FFMPVec:
     @property
     def state_m(self) -> torch.Tensor:
         """(N, 2, G, G) [older, newest] view of the frame window (contiguous iff W == 2)."""
-        return self.frames[:, self._wpos:self._wpos + 2]
+        if self.frame_window == 2:
+            return self.frames
+        return self.frames[self._wpos:self._wpos + 2].transpose(0, 1)
+
+    def _sm_strides(self):
+        """(env stride, frame stride) of state_m in floats, for ffmp_obs_t."""
+        G2 = self.cfg.grid * self.cfg.grid
+        return (2 * G2, G2) if self.frame_window == 2 else (G2, self.num_envs * G2)
 
     def _set_window(self, p: int) -> None:
         self._wpos = p
-        self._obs_c.state_m = self.frames.data_ptr() + p * self.cfg.grid * self.cfg.grid * 4
+        slot = self.num_envs * self.cfg.grid * self.cfg.grid * 4
+        self._obs_c.state_m = self.frames.data_ptr() + p * slot
 
     def _raster_bytes(self, n: int, full: bool) -> int:
         """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs

@@ -131,9 +131,11 @@ typedef struct ffmp_obs {
   float* lidar;     /* (N,L) ranges (+inf = no return, -inf = inside), NULL if L == 0 */
   float* flow;      /* (N,2,G,G) ego-frame velocity (m/s) of the disc covering each cell of the
                        newest frame (lowest disc index wins), 0 elsewhere; NULL unless cfg.flow */
-  int64_t state_m_stride; /* floats from env e's [older, newest] pair to env e+1's; 0 = 2*G*G
-                             (contiguous).  A frame window (N, W, G, G) is viewed with stride W*G*G
-                             and state_m pointing at the older slot (see FFMP_RASTER_NEWEST). */
+  int64_t state_m_stride;       /* floats from env e's older frame to env e+1's; 0 = 2*G*G */
+  int64_t state_m_frame_stride; /* floats from env e's older frame to its newest; 0 = G*G.
+                                   0/0 is the contiguous (N,2,G,G) layout.  A slot-major frame
+                                   window (W, N, G, G) uses G*G / N*G*G with state_m at the
+                                   older slot (see FFMP_RASTER_NEWEST). */
 } ffmp_obs_t;
 
 /* Per-step outputs (device pointers, N each). Flags are 0/1 bytes. */

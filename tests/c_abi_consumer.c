@@ -79,10 +79,11 @@ int main(void) {
                      (double*)dalloc(N * K * 4 * 8), (double*)dalloc(N * K * 8), (int32_t*)dalloc(N * 4),
                      (int32_t*)dalloc(N * 4), (float*)dalloc(N * rec * 4), (uint32_t*)dalloc(4),
                      NULL, NULL /* no terminal record / obs */};
-  float* frames = (float*)dalloc(N * W * G2 * 4); /* (N, W, G, G); state_m = slots [p, p+1] */
+  /* slot-major frame ring (W, N, G, G): state_m[e] = (slot p, slot p+1) of env e */
+  float* frames = (float*)dalloc((size_t)W * N * G2 * 4);
   ffmp_obs_t ob = {frames, (float*)dalloc(N * 2 * 4), (float*)dalloc(N * 2 * 4),
                    (float*)dalloc(N * 4), (float*)dalloc(N * G2 * 4), (float*)dalloc(N * 2 * 4),
-                   (float*)dalloc(N * L * 4), NULL, (int64_t)W * (int64_t)G2};
+                   (float*)dalloc(N * L * 4), NULL, (int64_t)G2, (int64_t)N * (int64_t)G2};
   ffmp_out_t out = {(float*)dalloc(N * 4), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N),
                     (uint8_t*)dalloc(N)};
   int64_t* act = (int64_t*)dalloc(N * 8);
@@ -104,9 +105,13 @@ int main(void) {
   float* mr = (float*)malloc(N * 4);
   int64_t* act_h = (int64_t*)malloc(N * 8);
   HIPCHK(hipStreamSynchronize(s));
-  /* the [older, newest] pairs of all envs: N rows of 2*G2 floats, W*G2 floats apart */
-#define COPY_PAIRS() \
-  HIPCHK(hipMemcpy2D(sm, 2 * G2 * 4, ob.state_m, (size_t)W * G2 * 4, 2 * G2 * 4, N, hipMemcpyDeviceToHost))
+  /* gather the [older, newest] pairs of all envs into sm (N, 2, G2): two strided plane copies */
+#define COPY_PAIRS()                                                                                  \
+  do {                                                                                              \
+    HIPCHK(hipMemcpy2D(sm, 2 * G2 * 4, ob.state_m, G2 * 4, G2 * 4, N, hipMemcpyDeviceToHost));      \
+    HIPCHK(hipMemcpy2D(sm + G2, 2 * G2 * 4, ob.state_m + (size_t)N * G2, G2 * 4, G2 * 4, N,         \
+                       hipMemcpyDeviceToHost));                                                     \
+  } while (0)
   COPY_PAIRS();
   for (int64_t e = 0; e < N; ++e) memcpy(prev_new + e * G2, sm + (e * 2 + 1) * G2, G2 * 4);
 
@@ -125,7 +130,7 @@ int main(void) {
      * wraps, when both frames are written at slot 0 */
     int32_t flags = FFMP_RASTER_NEWEST;
     if (++p > W - 2) { p = 0; flags = 0; }
-    ob.state_m = frames + (size_t)p * G2;
+    ob.state_m = frames + (size_t)p * N * G2;
     FFCHK(ffmp_raster_ex(&cfg, N, st.record, NULL, &ob, 0, flags, s));
     HIPCHK(hipStreamSynchronize(s));
     COPY_PAIRS();

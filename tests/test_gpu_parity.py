@@ -207,7 +207,7 @@ def test_pipelined_step_equals_serial(slices):
         t1, t2 = [], []
         ser.step(a, timing=t1)
         pip.step(a, timing=t2)
-        assert len(t1) == 1 and len(t2) == slices and sum(n for _, _, n in t2) == 83
+        assert len(t1) == 1 and len(t2) == slices and sum(r[2] for r in t2) == 83
     torch.cuda.synchronize()
     g1, g2 = gpu_snapshot(ser), gpu_snapshot(pip)
     for k in g1:

@@ -85,6 +85,7 @@ class FFMPVec:
         self.keep_terminal = bool(keep_terminal)
         self.placement = None
         self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
+        self.raster_shape_newest = (0, 0)  # the same for newest-only launches (frame ring)
         self.frame_window = self._pick_window(frame_window)
         self._wpos = 0  # frame slot of state_m[:, 0]
         self._alloc()
@@ -205,26 +206,35 @@ class FFMPVec:
     # after a real reset, for each candidate, and the fastest is kept.  Results are identical
     # for every shape.
     AUTOTUNE_MIN_BYTES = 256 << 20
+    # Newest-only launches (frame ring) move 2/3 of the bytes per block of a full launch, so they
+    # want bigger blocks (profiles/r01_window.txt: 16384-cell blocks 7.1 TB/s vs 6.7 at 4096);
+    # the two launch kinds are tuned independently from the same timed cycles.
     RASTER_SHAPES = (
         (4096, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN), (2048, _abi.RASTER_PLAIN | _abi.RASTER_XCD),
         (4096, _abi.RASTER_PLAIN | _abi.RASTER_XCD), (3072, _abi.RASTER_PLAIN | _abi.RASTER_XCD),
         (2048, _abi.RASTER_NT), (4096, _abi.RASTER_NT), (2048, _abi.RASTER_NT | _abi.RASTER_XCD),
+        (8192, _abi.RASTER_NT), (8192, _abi.RASTER_NT | _abi.RASTER_XCD), (16384, _abi.RASTER_NT),
+        (8192, _abi.RASTER_PLAIN), (16384, _abi.RASTER_PLAIN),
     )
 
-    def _raster_gbs_steady(self, steps: int = 3) -> float:
-        """Raster GB/s in the real regime: full steps (env kernel, then raster), raster
-        launches timed with HIP events.  (Back-to-back rasters alone can read up to 15 %
-        higher for some shapes than they sustain inside the step loop.)"""
-        from .config import bytes_per_env_step
+    def _raster_gbs_steady(self, steps: int = 3) -> Dict[bool, Tuple[float, float]]:
+        """Raster (GB/s, ms per launch) per launch kind (full: True, newest-only: False) in the
+        real regime: whole steps (env kernel, then raster), raster launches timed with HIP
+        events.  (Back-to-back rasters alone can read up to 15 % higher for some shapes than
+        they sustain inside the step loop.)"""
         a = torch.full((self.num_envs,), 10, dtype=torch.int64, device=self.device)
         self.step(a)
         t = []
         for _ in range(steps):
             self.step(a, timing=t)
         torch.cuda.synchronize(self.device)
-        ms = sum(x.elapsed_time(y) for x, y, *_ in t)
-        b = sum(r[3] for r in t)
-        return b / (ms * 1e-3) / 1e9
+        out = {}
+        for full in (True, False):
+            sel = [r for r in t if r[4] == full]
+            if sel:
+                ms = sum(r[0].elapsed_time(r[1]) for r in sel)
+                out[full] = (sum(r[3] for r in sel) / (ms * 1e-3) / 1e9, ms / len(sel))
+        return out
 
     # Placement retries.  Even the best shape runs ~15 % slower on a "slow" placement (e.g.
     # C3: 6.2-6.3 vs 7.1-7.3 TB/s), and allocating again while the first arena and a spacer
@@ -238,8 +248,8 @@ class FFMPVec:
 
     def _retry_placement(self) -> None:
         names = [n for n, _, _ in self._buffer_specs()]
-        keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names}, self.raster_shape,
-                 self.placement)]
+        keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
+                 (self.raster_shape, self.raster_shape_newest), self.placement)]
         spacers = []
         tries = [round(self.placement["gbs"], 1)]
         for k in range(self.PLACEMENT_RETRIES):
@@ -254,13 +264,13 @@ class FFMPVec:
             self._autotune_raster()
             tries.append(round(self.placement["gbs"], 1))
             keep.append((self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
-                         self.raster_shape, self.placement))
+                         (self.raster_shape, self.raster_shape_newest), self.placement))
         best = max(range(len(keep)), key=lambda i: keep[i][0])
-        _, buf, views, shape, placement = keep[best]
+        _, buf, views, shapes, placement = keep[best]
         self._arena_buf = buf
         for n, v in views.items():
             setattr(self, n, v)
-        self.raster_shape = shape
+        self.raster_shape, self.raster_shape_newest = shapes
         self.placement = dict(placement, placement_tries=tries, placement_kept=best)
         self._build_structs()
         del keep, spacers, views, buf
@@ -274,12 +284,26 @@ class FFMPVec:
         cyc = self.frame_window - 1  # whole window cycles: one full raster + W-2 newest-only
         steps = -(-steps // cyc) * cyc
         for shape in self.RASTER_SHAPES:
-            self.raster_shape = shape
+            self.raster_shape = self.raster_shape_newest = shape
             results.append((self._raster_gbs_steady(steps), shape))
-        gbs, shape = max(results)
-        self.raster_shape = shape
-        self.placement = {"shape": {"cells_per_block": shape[0], "flags": shape[1]}, "gbs": round(gbs, 1),
-                          "candidates": [[c, f, round(g, 1)] for g, (c, f) in results]}
+        best = {}
+        for kind in (True, False):
+            got = [(r[kind][0], r[kind][1], shape) for r, shape in results if kind in r]
+            if got:
+                best[kind] = max(got)
+        self.raster_shape = best[True][2]
+        self.raster_shape_newest = best[False][2] if False in best else self.raster_shape
+        # the cycle's bandwidth with the chosen shapes: one full launch + W-2 newest-only ones
+        n_new = self.frame_window - 2
+        b = self._raster_bytes(self.num_envs, True) + n_new * self._raster_bytes(self.num_envs, False)
+        ms = best[True][1] + (n_new * best[False][1] if n_new else 0.0)
+        gbs = b / (ms * 1e-3) / 1e9
+        self.placement = {"shape": {"cells_per_block": self.raster_shape[0], "flags": self.raster_shape[1]},
+                          "shape_newest": ({"cells_per_block": self.raster_shape_newest[0],
+                                            "flags": self.raster_shape_newest[1]} if n_new else None),
+                          "gbs": round(gbs, 1),
+                          "candidates": [[c, f] + [round(r[k][0], 1) for k in (True, False) if k in r]
+                                         for r, (c, f) in results]}
         if self._arena_buf is not None:
             self._arena_buf.zero_()
         self._needs_reset = True
@@ -357,13 +381,13 @@ class FFMPVec:
         return n * per
 
     def _raster_launch(self, full: bool, mask=None, timing: Optional[list] = None) -> None:
-        flags = self.raster_shape[1] | (0 if full else _abi.RASTER_NEWEST)
+        cpb, flags = self.raster_shape if full else self.raster_shape_newest
+        flags |= 0 if full else _abi.RASTER_NEWEST
         if timing is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), self.num_envs, self.record.data_ptr(), _ptr(mask),
-                                           C.byref(self._obs_c), self.raster_shape[0], flags, self._stream()),
-                   "ffmp_raster")
+                                           C.byref(self._obs_c), cpb, flags, self._stream()), "ffmp_raster")
         if timing is not None:
             e1.record()
             timing.append((e0, e1, self.num_envs, self._raster_bytes(self.num_envs, full), full))

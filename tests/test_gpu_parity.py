@@ -234,11 +234,31 @@ def test_raster_shapes_identical():
         assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), shape
 
 
+def test_newest_only_shapes_identical():
+    """Newest-only launches (frame ring) are bit-identical for every shape, too."""
+    cfg = FFMPConfig(grid=64, n_obst=24, n_beams=0, moving=True, obst_rmax=0.8, max_steps=3, seed=78)
+    ref = None
+    for shape in FFMPVec.RASTER_SHAPES:
+        env = FFMPVec(29, cfg, device="cuda:0", autotune=False, frame_window=5)
+        env.raster_shape = env.raster_shape_newest = shape
+        env.reset()
+        gen = torch.Generator(device="cuda:0").manual_seed(9)
+        outs = []
+        for _ in range(9):
+            o, _, _, _ = env.step(torch.randint(0, 28, (29,), device="cuda:0", generator=gen))
+            outs.append((o["state_m"].clone(), o["potential"].clone()))
+        if ref is None:
+            ref = outs
+        for (a, b), (c, d) in zip(outs, ref):
+            assert torch.equal(a, c) and torch.equal(b, d), shape
+
+
 def test_autotune_picks_a_candidate():
     cfg = FFMPConfig(grid=128, n_obst=8, n_beams=0, seed=3)
     env = FFMPVec(8192, cfg, device="cuda:0")  # 8192 x 3 x 64 KiB planes > AUTOTUNE_MIN_BYTES
     assert env.placement is not None
     assert tuple(env.raster_shape) in FFMPVec.RASTER_SHAPES
+    assert env.frame_window == 8 and tuple(env.raster_shape_newest) in FFMPVec.RASTER_SHAPES
     with pytest.raises(RuntimeError):
         env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))  # autotune leaves it un-reset
     env.reset()

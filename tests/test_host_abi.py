@@ -127,6 +127,9 @@ def test_bytes_model():
     b = bytes_per_env_step(preset("C3"))
     assert b["raster"] == 12 * 256 * 256 + 4 * (16 + 12 * 16)
     assert bytes_per_env_step(preset("C3", flow=True))["raster"] == 20 * 256 * 256 + 4 * (16 + 12 * 16)
+    # frame window W: the older frame is written on 1 step in W-1 (plus resets, counted by bench.py)
+    assert bytes_per_env_step(preset("C3"), window=8)["raster"] == 8 * 65536 + (4 * 65536) // 7 + 4 * (16 + 12 * 16)
+    assert bytes_per_env_step(preset("C3"), window=2)["raster"] == b["raster"]
     assert b["total"] > b["raster"]
 
 

@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--flow", action="store_true", help="also raster the BEV motion-flow planes (not a BASELINE config)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--cpu-procs", type=int, default=16,
+                   help="processes of the parallel CPU baseline (SURVEY 8d (ii); capped at the host's CPUs, 0 = skip)")
+    p.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
     p.add_argument("--frame-window", type=int, default=None,
@@ -73,6 +76,52 @@ def cpu_baseline(cfg, seconds: float):
                       f"OracleVecEnv, 1 process / 1 thread"}
 
 
+def cpu_worker(spec: str) -> None:
+    """Child of the parallel CPU baseline: one oracle shard for `seconds`, prints its count."""
+    import numpy as np
+    from flow_field_based_motion_planner_amd.config import FFMPConfig
+    from oracle.ffmp_oracle import OracleVecEnv
+    d = json.loads(spec)
+    cfg = FFMPConfig(**d["cfg"])
+    n = d["envs"]
+    env = OracleVecEnv(cfg, n, env_offset=d["offset"])
+    env.reset()
+    rng = np.random.default_rng(d["offset"])
+    env.step(rng.integers(0, 28, n))
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < d["seconds"]:
+        env.step(rng.integers(0, 28, n))
+        steps += 1
+    print(json.dumps({"env_steps": n * steps, "seconds": time.perf_counter() - t0}), flush=True)
+
+
+def cpu_baseline_parallel(cfg, seconds: float, procs: int):
+    """`procs` single-threaded processes, one oracle shard of 4 envs each, run
+    concurrently as child processes; aggregate env-steps/s."""
+    import subprocess
+    procs = max(1, min(procs, os.cpu_count() or 1))
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    kids = []
+    for r in range(procs):
+        spec = json.dumps({"cfg": cfg.to_dict(), "envs": 4, "offset": 4 * r, "seconds": seconds})
+        kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", spec],
+                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, text=True))
+    rate, done = 0.0, 0
+    for k in kids:
+        out, _ = k.communicate(timeout=seconds * 4 + 120)
+        lines = [l for l in out.splitlines() if l.startswith("{")]
+        if k.returncode == 0 and lines:
+            d = json.loads(lines[-1])
+            rate += d["env_steps"] / d["seconds"]
+            done += 1
+    if done != procs:
+        return None
+    return {"value": rate, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes x 4 envs of the same config, {seconds:.0f} s each, NumPy oracle, "
+                      f"1 thread per process"}
+
+
 def load_traffic(workload: str, n_envs: int, window: int):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
@@ -90,6 +139,9 @@ def load_traffic(workload: str, n_envs: int, window: int):
 
 def main():
     args = parse()
+    if args.cpu_worker is not None:
+        cpu_worker(args.cpu_worker)
+        return
     import torch
     import torch.distributed as dist
     from flow_field_based_motion_planner_amd.config import PRESETS, bytes_per_env_step, preset
@@ -202,6 +254,8 @@ def main():
         }
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            if args.cpu_procs > 0:
+                out["cpu_baseline_parallel"] = cpu_baseline_parallel(cfg, min(args.cpu_seconds, 10.0), args.cpu_procs)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -42,7 +42,6 @@ import os
 import sys
 import tempfile
 import types
-import unittest.mock  # noqa: F401  (inert stand-ins for the loop's ROS / logging objects)
 
 import numpy as np
 

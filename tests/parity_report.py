@@ -6,8 +6,6 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 from tests.parity_util import exact_report, gpu_snapshot, oracle_snapshot  # noqa: E402
 from tests.test_gpu_parity import CASES, _run  # noqa: E402

@@ -4,7 +4,6 @@ lookup, footprint consistency, truncation/auto-reset, lidar geometry, sharding."
 import math
 
 import numpy as np
-import pytest
 
 from flow_field_based_motion_planner_amd.config import FFMPConfig
 from oracle import ffmp_oracle as O

@@ -3,7 +3,6 @@ each, in one process (same box).  Usage: python tools/alloc_ab.py [trials]"""
 import gc
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402

@@ -8,7 +8,6 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from flow_field_based_motion_planner_amd import _abi  # noqa: E402
 from flow_field_based_motion_planner_amd.config import PRESETS, bytes_per_env_step, preset  # noqa: E402
 from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 

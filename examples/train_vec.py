@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--target-every", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--save", default="")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
 
     dev = torch.device("cuda:0")
@@ -52,7 +53,11 @@ def main():
     losses, updates = [], 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for step in range(args.steps):
+    t_warm = None
+    for step in range(args.warmup + args.steps):
+        if step == args.warmup:
+            torch.cuda.synchronize()
+            t_warm = time.perf_counter()
         action = brain.decide_action(obs, tracker.episode)
         brain.memory.push_begin()
         obs, reward, done, info = env.step(action)
@@ -67,10 +72,12 @@ def main():
                 if updates % args.target_every == 0:
                     brain.update_target_q_network()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    dt = t1 - t_warm
     env.check_errors()
     summ = tracker.summary()
-    out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "envs": args.envs, "steps": args.steps,
+    out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "warmup_seconds": t_warm - t0,
+           "envs": args.envs, "steps": args.steps,
            "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],
            "replay_bytes": brain.memory.hbm_bytes(), "replay_len": len(brain.memory), **summ}
     print(json.dumps(out))

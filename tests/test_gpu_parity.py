@@ -300,3 +300,21 @@ def test_frame_window_equals_contiguous(window):
     b.load_state_dict(sd)
     assert torch.equal(a.state_m, b.state_m)
 
+
+
+def test_limits_parity():
+    """The ABI's maxima at once: K = 64 discs, L = 1024 beams, a 1024^2 grid, global env indices
+    above 2^32 (the Philox counter's high word), a 3-frame ring — against the oracle."""
+    cfg = FFMPConfig(grid=1024, n_obst=64, n_beams=1024, moving=True, max_steps=4, obst_rmax=0.8,
+                     obst_vmax=1.5, seed=2 ** 63 + 12345)
+    env, ref, problems, counts = _run(cfg, 3, 6, env_offset=2 ** 32 + 7, frame_window=3)
+    assert not problems, "\n".join(problems[:10])
+    assert counts["done"] > 0
+
+
+def test_single_env_and_ragged_counts():
+    """n = 1 and n not a multiple of the 4-env / 64-lane groupings, through the ring."""
+    for n in (1, 3, 65, 130):
+        cfg = FFMPConfig(grid=32, n_obst=5, n_beams=70, moving=True, max_steps=3, seed=n)
+        env, ref, problems, _ = _run(cfg, n, 5, frame_window=4)
+        assert not problems, (n, problems[:5])

@@ -1,0 +1,41 @@
+"""Where the env kernel's time goes at C3 size: time ffmp_step_state alone for variants of the
+C3 config (no lidar, no obstacles, static obstacles, footprint-only collisions, fewer beams)."""
+import gc
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from flow_field_based_motion_planner_amd.config import preset  # noqa: E402
+from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
+
+n = 32768
+variants = {
+    "C3": {},
+    "L=0 (no lidar)": dict(n_beams=0),
+    "L=64": dict(n_beams=64),
+    "K=0": dict(n_obst=0),
+    "K=4": dict(n_obst=4),
+    "static": dict(moving=False),
+    "footprint only": dict(collide_mode=1),
+    "lidar only": dict(collide_mode=2),
+    "G=64 (same K, L)": dict(grid=64),
+}
+for name, kw in variants.items():
+    env = FFMPVec(n, preset("C3", **kw), device="cuda:0", autotune=False, frame_window=2, potential=False)
+    env.reset()
+    acts = torch.randint(0, 28, (60, n), device="cuda:0")
+    for k in range(10):
+        env.step_state(acts[k])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    ev[0].record()
+    for k in range(10, 60):
+        env.step_state(acts[k])
+    ev[1].record()
+    torch.cuda.synchronize()
+    print(f"{name:20s}: env kernel {ev[0].elapsed_time(ev[1]) / 50 * 1000:7.1f} us", flush=True)
+    del env
+    gc.collect()
+    torch.cuda.empty_cache()

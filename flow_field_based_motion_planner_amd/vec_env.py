@@ -18,7 +18,9 @@ extras: potential (N,G,G), grad (N,2), lidar (N,L).
 
 Every entry point goes through the HIP library; there is no CPU path.  The
 returned obs dict holds the env's own device buffers (overwritten in place by
-the next step/reset) unless `copy=True`.
+the next step/reset) unless `copy=True`.  With a frame ring (frame_window > 2)
+`state_m` is a view of the current pair of ring slots, so take it from each
+step's return value (or `env.state_m`) rather than keeping the first one.
 """
 from __future__ import annotations
 

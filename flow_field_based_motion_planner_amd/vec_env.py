@@ -199,7 +199,7 @@ class FFMPVec:
             nb = self._nbytes(shape, dtype)
             setattr(self, name, self._arena_buf[base + o:base + o + nb].view(dtype).view(shape))
 
-    # Raster launch-shape autotune (profiles/r01_placement.txt, r01_raster_shapes.txt).  The
+    # Raster launch-shape autotune (profiles/r01_placement.txt, r01_raster_tuning.txt).  The
     # raster's three concurrent 16-B store streams run anywhere from 5.7 to 7.3 TB/s depending
     # on where the planes land in HBM (fixed per allocation, identical virtual layouts) and on
     # the launch shape, and the best shape differs between allocations (e.g. 4096-cell blocks

@@ -443,7 +443,9 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const bool has = lane < K;
   const float4 oc = has ? s_cur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 op = has ? s_prev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float rc = oc.w + cfg.rho0_f + cfg.cull_margin_f;  // potential reach (covers occupancy)
+  const bool with_pot = pot != nullptr;  // uniform: skip the potential entirely without a plane
+  // potential reach (covers occupancy), or the occupancy reach alone without a potential plane
+  const float rc = oc.w + (with_pot ? cfg.rho0_f : 0.0f) + cfg.cull_margin_f;
   const float rp = op.w + cfg.cull_margin_f;               // occupancy reach
   const float rc2 = rc * rc, rp2 = rp * rp;
   // lanes 0..3: corners of the current frame, 4..7: previous frame
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
     for (int u = 0; u < 4; ++u) {
       occp[u] = (walls_p && outside_world(cfg, hp, ex, ey[u])) ? 1.0f : 0.0f;
       occc[u] = (walls_c && outside_world(cfg, hc, ex, ey[u])) ? 1.0f : 0.0f;
-      U[u] = attractive(cfg, ex, ey[u], gx, gy);
+      U[u] = with_pot ? attractive(cfg, ex, ey[u], gx, gy) : 0.0f;
     }
     for (uint64_t m = mp; m; m &= m - 1) {
       const float4 o = s_prev[__builtin_ctzll(m)];
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
           fy[u] = s_vel[k].y;
           fset[u] = true;
         }
-        U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
+        if (with_pot) U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
       }
     }
     if (write_old) store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);

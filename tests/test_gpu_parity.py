@@ -318,3 +318,22 @@ def test_single_env_and_ragged_counts():
         cfg = FFMPConfig(grid=32, n_obst=5, n_beams=70, moving=True, max_steps=3, seed=n)
         env, ref, problems, _ = _run(cfg, n, 5, frame_window=4)
         assert not problems, (n, problems[:5])
+
+
+def test_no_potential_same_frames():
+    """Without a potential plane the raster skips the potential math and culls with the
+    occupancy reach only: frames (and flow) stay bit-identical to the full raster's."""
+    cfg = FFMPConfig(grid=64, n_obst=24, n_beams=8, moving=True, obst_rmax=0.6, obst_vmax=1.5, world_half=3.0,
+                     max_steps=6, flow=True, seed=43)
+    for w in (2, 4):
+        a = FFMPVec(33, cfg, device="cuda:0", frame_window=w)
+        b = FFMPVec(33, cfg, device="cuda:0", frame_window=w, potential=False)
+        a.reset()
+        b.reset()
+        rng = np.random.default_rng(w)
+        for _ in range(10):
+            act = torch.as_tensor(rng.integers(0, 28, 33), device="cuda:0")
+            oa, _, _, _ = a.step(act)
+            ob, _, _, _ = b.step(act)
+            assert torch.equal(oa["state_m"], ob["state_m"]) and torch.equal(oa["flow"], ob["flow"])
+            assert "potential" not in ob

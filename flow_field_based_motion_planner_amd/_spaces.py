@@ -4,7 +4,7 @@ import numpy as np
 
 try:  # pragma: no cover - gym absent here
     import gym as _gym
-    from gym.spaces import Box, Dict  # noqa: F401
+    from gym.spaces import Box, Dict, Discrete, MultiDiscrete  # noqa: F401
     GymEnvBase = _gym.Env
 except Exception:  # noqa: BLE001
     _gym = None
@@ -25,6 +25,31 @@ except Exception:  # noqa: BLE001
 
         def __repr__(self):
             return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+    class Discrete(object):
+        def __init__(self, n):
+            self.n = int(n)
+            self.shape = ()
+            self.dtype = np.dtype(np.int64)
+
+        def contains(self, x):
+            return 0 <= int(x) < self.n
+
+        def __repr__(self):
+            return f"Discrete({self.n})"
+
+    class MultiDiscrete(object):
+        def __init__(self, nvec):
+            self.nvec = np.asarray(nvec, dtype=np.int64)
+            self.shape = self.nvec.shape
+            self.dtype = np.dtype(np.int64)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all((x >= 0) & (x < self.nvec)))
+
+        def __repr__(self):
+            return f"MultiDiscrete({self.nvec.tolist()[:4]}{'...' if self.nvec.size > 4 else ''})"
 
     class Dict(object):
         def __init__(self, spaces):

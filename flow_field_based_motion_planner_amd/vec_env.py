@@ -27,6 +27,7 @@ from __future__ import annotations
 import ctypes as C
 from typing import Dict, Optional, Tuple, Union
 
+import numpy as np
 import torch
 
 from . import _abi
@@ -508,6 +509,75 @@ class FFMPVec:
             info = {k: v.clone() for k, v in info.items()}
             return self._obs_out(True), self.reward.clone(), self.done.clone(), info
         return self.obs, self.reward, self.done, info
+
+    # ------------------------------------------------ gym.vector.VectorEnv surface
+    is_vector_env = True
+
+    @property
+    def single_action_space(self):
+        """The action id train.py feeds to RobotAction.commander (train.py:343-345, 668-673);
+        the reference's Box (ffmp.py:29-32) describes the (v, w) it maps to."""
+        from ._spaces import Discrete
+        return Discrete(28)
+
+    @property
+    def action_space(self):
+        from ._spaces import MultiDiscrete
+        return MultiDiscrete([28] * self.num_envs)
+
+    def _obs_space(self, lead):
+        """Keys/dtypes of the train.py consumer contract (train.py:543-557), bounds per key."""
+        from ._spaces import Box, Dict as DictSpace
+        G, L = self.cfg.grid, self.cfg.n_beams
+        inf = np.inf
+
+        def box(lo, hi, shape):
+            lo = np.broadcast_to(np.asarray(lo, dtype=np.float32), lead + shape)
+            hi = np.broadcast_to(np.asarray(hi, dtype=np.float32), lead + shape)
+            return Box(lo, hi, dtype=np.float32)
+
+        sp = {"state_m": box(0.0, 255.0, (2, G, G)),
+              "state_g": box([0.0, -np.pi], [inf, np.pi], (2,)),   # [dist, orient]
+              "state_v": box([0.0, -np.pi], [inf, np.pi], (2,)),   # [|dxy|, wrap(dyaw)] per step
+              "state_t": box(0.0, inf, (1,)),
+              "grad": box(-inf, inf, (2,))}
+        if self.potential is not None:
+            sp["potential"] = box(0.0, inf, (G, G))
+        if L:
+            sp["lidar"] = box(-inf, inf, (L,))
+        if self.flow is not None:
+            sp["flow"] = box(-inf, inf, (2, G, G))
+        return DictSpace(sp)
+
+    @property
+    def single_observation_space(self):
+        return self._obs_space(())
+
+    @property
+    def observation_space(self):
+        return self._obs_space((self.num_envs,))
+
+    def seed(self, seed: int) -> None:
+        """gym 0.17-style: the seed of the next full reset()."""
+        self.cfg = self.cfg.replace(seed=int(seed))
+        self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
+
+    def step_async(self, actions) -> None:
+        self._pending_actions = actions
+
+    def step_wait(self, **kw):
+        a, self._pending_actions = self._pending_actions, None
+        if a is None:
+            raise RuntimeError("step_wait() without step_async()")
+        return self.step(a, **kw)
+
+    def close(self) -> None:
+        """Release the device buffers (the object is unusable afterwards)."""
+        self._needs_reset = True
+        for name, _, _ in self._buffer_specs():
+            setattr(self, name, None)
+        self._arena_buf = None
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ utilities
     def check_errors(self) -> None:

@@ -191,3 +191,30 @@ def test_no_potential_mode():
     o = v.reset()
     assert "potential" not in o and v.potential is None
     v.step(torch.zeros(3, dtype=torch.int64, device="cuda:0"))
+
+
+def test_vector_env_surface():
+    """gym.vector.VectorEnv-style attributes and step_async / step_wait on FFMPVec."""
+    cfg = FFMPConfig(grid=64, n_obst=4, n_beams=16, moving=True, seed=12)
+    a = P.FFMPVec(6, cfg, device="cuda:0")
+    b = P.FFMPVec(6, cfg, device="cuda:0")
+    assert a.is_vector_env and a.num_envs == 6
+    assert a.single_action_space.n == 28 and a.action_space.shape == (6,)
+    so, bo = a.single_observation_space, a.observation_space
+    assert so["state_m"].shape == (2, 64, 64) and bo["state_m"].shape == (6, 2, 64, 64)
+    assert bo["lidar"].shape == (6, 16) and "potential" in bo.spaces
+    oa = a.reset()
+    b.seed(cfg.seed)
+    b.reset()
+    for k in so.spaces:
+        assert so[k].contains(oa[k][0].cpu().numpy()), k
+    act = torch.randint(0, 28, (6,), device="cuda:0")
+    ra = a.step(act)
+    b.step_async(act)
+    rb = b.step_wait()
+    assert torch.equal(ra[0]["state_m"], rb[0]["state_m"]) and torch.equal(ra[1], rb[1])
+    with pytest.raises(RuntimeError):
+        b.step_wait()
+    b.close()
+    with pytest.raises(RuntimeError):
+        b.step(act)

@@ -22,7 +22,10 @@ variants = {
     "lidar only": dict(collide_mode=2),
     "G=64 (same K, L)": dict(grid=64),
 }
+only = sys.argv[1:]  # optional variant names to run
 for name, kw in variants.items():
+    if only and name not in only:
+        continue
     env = FFMPVec(n, preset("C3", **kw), device="cuda:0", autotune=False, frame_window=2, potential=False)
     env.reset()
     acts = torch.randint(0, 28, (60, n), device="cuda:0")

@@ -16,6 +16,8 @@ variants = {
     "L=0 (no lidar)": dict(n_beams=0),
     "L=64": dict(n_beams=64),
     "K=0": dict(n_obst=0),
+    "K=0,L=0": dict(n_obst=0, n_beams=0),
+    "K=0,L=0,no collide": dict(n_obst=0, n_beams=0, collide_mode=0),
     "K=4": dict(n_obst=4),
     "static": dict(moving=False),
     "footprint only": dict(collide_mode=1),

@@ -182,7 +182,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
             raise FFMPBackendError(f"ABI layout mismatch (item {k}): library {got}, ctypes {v}")
 
 
-TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES = 1, 2, 3, 4
+TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES, TUNE_ENV_LANES = 1, 2, 3, 4, 5
 RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
 
 

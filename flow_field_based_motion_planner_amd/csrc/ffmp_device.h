@@ -227,23 +227,32 @@ FFMP_DEV bool occupied_cell(const ffmp_cfg_t& cfg, const FrameHdr& h, const floa
 // wall farther than that (|dir| <= 1), so skipping them leaves every range bit-identical.
 constexpr double kLidarCullMargin = 1e-6;
 
+// Ballot over the `lpe` lanes that serve this lane's env (an env owns lanes [g*lpe, g*lpe+lpe) of
+// the wave; bit k of the result = its lane k).  lpe is 16, 32 or 64 (wave-uniform).
+FFMP_DEV uint64_t group_ballot(bool pred, int lpe) {
+  const uint64_t m = __ballot(pred);
+  if (lpe == 64) return m;
+  const int base = (int)(threadIdx.x & 63) & ~(lpe - 1);
+  return (m >> base) & ((1ull << lpe) - 1ull);
+}
+
 struct LidarScene {
   uint64_t mask;
   bool inside;
   bool wxp, wxn, wyp, wyn;
 };
 
-// Call from every lane of the env's wave; lane k < K holds disc k.
+// Call from every lane of the env's lane group; its lane k < K holds disc k.
 FFMP_DEV LidarScene lidar_scene(const ffmp_cfg_t& cfg, double x, double y, double ox, double oy, double r,
-                                bool has) {
+                                bool has, int lpe) {
   const double rx = ox - x, ry = oy - y;
   const double rr = rx * rx + ry * ry;
   const bool in = has && (rr <= r * r);
   const double reach = cfg.lidar_max + kLidarCullMargin;
   const bool act = has && (in || !(sqrt(rr) - r > reach));
   LidarScene sc;
-  sc.mask = __ballot(act);
-  sc.inside = __any(in);
+  sc.mask = group_ballot(act, lpe);
+  sc.inside = group_ballot(in, lpe) != 0;
   const double W = cfg.world_half;
   sc.wxp = (W - x) <= reach;
   sc.wxn = (x + W) <= reach;

@@ -1,7 +1,7 @@
 // ffmp_kernels.hip — CDNA4 (gfx950) kernels + C ABI of libffmp.
 //
 // Kernels
-//   env_kernel<MODE>   one 64-lane wave per env: action -> unicycle integrate,
+//   env_kernel<MODE>   16/32/64 lanes per env (1-4 envs per wave): action -> unicycle integrate,
 //                      obstacle motion, lidar (lane per beam), footprint
 //                      collision (lane per footprint cell), goal/reward/done,
 //                      truncation, auto-reset (Philox), gradient lookup, and the
@@ -67,12 +67,14 @@ int check_cfg(const ffmp_cfg_t* c) {
 
 // Launch-shape tuning.  Defaults are the measured best on MI355X (profiles/r01_*);
 // ffmp_set_tuning() (or the FFMP_RASTER_CPB / FFMP_RASTER_NT / FFMP_RASTER_XCD /
-// FFMP_ENV_WAVES environment variables, read once) overrides them for tuning sweeps.
+// FFMP_ENV_WAVES / FFMP_ENV_LANES environment variables, read once) overrides them for tuning
+// sweeps.
 struct Tuning {
   int cells_per_block = 4096;  // raster cells per block (multiple of 1024)
   int nontemporal = -1;        // raster store flavour: -1 by plane size, 0 plain, 1 nontemporal
   int xcd_remap = 0;           // 1: each XCD walks its own contiguous range of (env, tile) blocks
-  int env_waves = 1;           // envs (waves) per env_kernel block: 1 or 4
+  int env_waves = 1;           // waves per env_kernel block: 1 or 4
+  int env_lanes = 0;           // lanes per env: 0 = auto (>= K, more for many lidar beams)
 };
 
 Tuning& tuning() {
@@ -85,6 +87,10 @@ Tuning& tuning() {
     if (const char* v = getenv("FFMP_RASTER_NT")) r.nontemporal = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("FFMP_RASTER_XCD")) r.xcd_remap = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("FFMP_ENV_WAVES")) r.env_waves = atoi(v) == 4 ? 4 : 1;
+    if (const char* v = getenv("FFMP_ENV_LANES")) {
+      const int l = atoi(v);
+      r.env_lanes = (l == 16 || l == 32 || l == 64) ? l : 0;
+    }
     return r;
   }();
   return t;
@@ -134,23 +140,30 @@ FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const Fra
   }
 }
 
-template <int MODE, int kEnvWaves>
+// LPE lanes per env (16, 32 or 64 >= K): a wave serves 64 / LPE envs, so the per-env scalar
+// float64 work (integrator, trig, goal, reward, record header) is issued once per 64/LPE envs
+// instead of once per env; lane k of an env's group holds its obstacle k, beams and footprint
+// cells are strided over the group's lanes.
+template <int MODE, int kEnvWaves, int LPE>
 __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                  const int64_t* __restrict__ action,
                                                  const uint8_t* __restrict__ mask, int32_t initial,
                                                  ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
+  static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
+  constexpr int EPW = 64 / LPE;  // envs per wave
   __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
       s_ora[kEnvWaves][FFMP_MAX_OBST];
   __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
 
   const int wv = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * kEnvWaves + wv;
-  const int lane = threadIdx.x & 63;
-  double* s_ox = s_oxa[wv];
-  double* s_oy = s_oya[wv];
-  double* s_or = s_ora[wv];
-  float4* s_ecur = s_ecura[wv];
-  float4* s_eprev = s_epreva[wv];
+  const int grp = (threadIdx.x & 63) / LPE;
+  const int64_t e = ((int64_t)blockIdx.x * kEnvWaves + wv) * EPW + grp;
+  const int lane = threadIdx.x & (LPE - 1);  // lane within the env's group
+  double* s_ox = s_oxa[wv] + grp * LPE;
+  double* s_oy = s_oya[wv] + grp * LPE;
+  double* s_or = s_ora[wv] + grp * LPE;
+  float4* s_ecur = s_ecura[wv] + grp * LPE;
+  float4* s_eprev = s_epreva[wv] + grp * LPE;
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
 
@@ -224,21 +237,21 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
     // ---- collision: footprint on the current occupancy (ffmp.py:85-105) ----
     bool c_foot = false;
     if (cfg.collide_mode & FFMP_COLLIDE_FOOTPRINT) {
-      for (int f = lane; f < cfg.n_foot; f += 64)
+      for (int f = lane; f < cfg.n_foot; f += LPE)
         c_foot |= occupied_cell(cfg, hcur, s_ecur, K, ic + cfg.foot_di[f], ic + cfg.foot_dj[f]);
     }
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
-    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst);
-    for (int l = lane; l < L; l += 64) {
+    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
+    for (int l = lane; l < L; l += LPE) {
       const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
                                   s_ox, s_oy, s_or);
       const float rf = (float)r;
       ob.lidar[e * L + l] = rf;
       c_lidar |= beam_collides(rf, cfg.robot_r);
     }
-    c_foot = __any(c_foot);
-    c_lidar = __any(c_lidar) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
+    c_foot = group_ballot(c_foot, LPE) != 0;
+    c_lidar = (group_ballot(c_lidar, LPE) != 0) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
     col = c_foot || c_lidar;
     // ---- is_goal / reward / is_done (ffmp.py:120-164), truncation (train.py:607) ----
     goal = dist < cfg.goal_thr;
@@ -290,8 +303,8 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
       ob.state_g[e * 2 + 0] = (float)dist;
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
-    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst);
-    for (int l = lane; l < L; l += 64) {
+    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
+    for (int l = lane; l < L; l += LPE) {
       const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
                                   s_ox, s_oy, s_or);
       ob.lidar[e * L + l] = (float)r;
@@ -307,7 +320,8 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
       const int dj = (lane == 2) ? 1 : (lane == 3) ? -1 : 0;
       U = potential_cell(cfg, s_ecur, K, ge.x, ge.y, ic + di, ic + dj);
     }
-    const float Uxp = __shfl(U, 0), Uxm = __shfl(U, 1), Uyp = __shfl(U, 2), Uym = __shfl(U, 3);
+    const float Uxp = __shfl(U, 0, LPE), Uxm = __shfl(U, 1, LPE), Uyp = __shfl(U, 2, LPE),
+                Uym = __shfl(U, 3, LPE);
     if (lane == 0) {
       ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
       ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
@@ -703,6 +717,31 @@ static int check_episode(const ffmp_episode_t* ep) {
   return FFMP_OK;
 }
 
+template <int MODE, int W, int LPE>
+void launch_env_t(const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action, const uint8_t* mask,
+                  int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob, const ffmp_out_t& o,
+                  hipStream_t s) {
+  const int64_t per_block = (int64_t)W * (64 / LPE);
+  const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
+  hipLaunchKernelGGL((env_kernel<MODE, W, LPE>), dim3(blocks), dim3(64 * W), 0, s, cfg, n, env_offset, action, mask,
+                     initial, st, ob, o);
+}
+
+template <int W>
+void launch_env_lpe(int mode, int lpe, const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action,
+                    const uint8_t* mask, int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob,
+                    const ffmp_out_t& o, hipStream_t s) {
+  if (mode == kEnvMode_Step) {
+    if (lpe == 16) launch_env_t<kEnvMode_Step, W, 16>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+    else if (lpe == 32) launch_env_t<kEnvMode_Step, W, 32>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+    else launch_env_t<kEnvMode_Step, W, 64>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+  } else {
+    if (lpe == 16) launch_env_t<kEnvMode_Reset, W, 16>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+    else if (lpe == 32) launch_env_t<kEnvMode_Reset, W, 32>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+    else launch_env_t<kEnvMode_Reset, W, 64>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+  }
+}
+
 // ============================================================================
 // C ABI
 // ============================================================================
@@ -732,6 +771,12 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       if (value != 1 && value != 4) return fail(FFMP_E_ARG, "env waves must be 1 or 4");
       prev = t.env_waves;
       t.env_waves = value;
+      return prev;
+    case FFMP_TUNE_ENV_LANES:
+      if (value != 0 && value != 16 && value != 32 && value != 64)
+        return fail(FFMP_E_ARG, "env lanes must be 0 (auto), 16, 32 or 64");
+      prev = t.env_lanes;
+      t.env_lanes = value;
       return prev;
     default:
       return fail(FFMP_E_ARG, "unknown tuning key %d", key);
@@ -799,24 +844,17 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
   if (n == 0) return FFMP_OK;
   if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
   ffmp_out_t o = out ? *out : ffmp_out_t{};
-  hipStream_t s = (hipStream_t)stream;
-  const int waves = tuning().env_waves;
-  const unsigned grid1 = (unsigned)n, grid4 = (unsigned)((n + 3) / 4);
-  if (mode == kEnvMode_Step) {
-    if (waves == 4)
-      hipLaunchKernelGGL((env_kernel<kEnvMode_Step, 4>), dim3(grid4), dim3(256), 0, s, *cfg, n, env_offset, action,
-                         mask, initial, *state, *obs, o);
-    else
-      hipLaunchKernelGGL((env_kernel<kEnvMode_Step, 1>), dim3(grid1), dim3(64), 0, s, *cfg, n, env_offset, action,
-                         mask, initial, *state, *obs, o);
-  } else {
-    if (waves == 4)
-      hipLaunchKernelGGL((env_kernel<kEnvMode_Reset, 4>), dim3(grid4), dim3(256), 0, s, *cfg, n, env_offset, action,
-                         mask, initial, *state, *obs, o);
-    else
-      hipLaunchKernelGGL((env_kernel<kEnvMode_Reset, 1>), dim3(grid1), dim3(64), 0, s, *cfg, n, env_offset, action,
-                         mask, initial, *state, *obs, o);
-  }
+  const Tuning& tu = tuning();
+  // lanes per env: at least K (lane k holds disc k); with many beams more lanes keep the lidar
+  // loop short (profiles/r01_env_kernel.txt: C3 with L = 180 is fastest at 32, L = 64 at 16)
+  const int need = cfg->n_obst <= 16 ? 16 : cfg->n_obst <= 32 ? 32 : 64;
+  const int want_l = cfg->n_beams <= 128 ? 16 : cfg->n_beams <= 256 ? 32 : 64;
+  const int autol = need > want_l ? need : want_l;
+  const int lpe = tu.env_lanes ? (tu.env_lanes >= need ? tu.env_lanes : need) : autol;
+  if (tu.env_waves == 4)
+    launch_env_lpe<4>(mode, lpe, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, (hipStream_t)stream);
+  else
+    launch_env_lpe<1>(mode, lpe, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, (hipStream_t)stream);
   return check_launch(mode == kEnvMode_Step ? "ffmp_step_state" : "ffmp_reset");
 }
 

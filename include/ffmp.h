@@ -161,7 +161,8 @@ int64_t ffmp_layout(int32_t which);
 #define FFMP_TUNE_RASTER_CPB 1  /* raster cells per block: multiple of 1024; 0 = default   */
 #define FFMP_TUNE_RASTER_NT 2   /* raster stores: 0 by plane size, 1 plain, 2 nontemporal  */
 #define FFMP_TUNE_RASTER_XCD 3  /* 1: XCD-aware block remap                                */
-#define FFMP_TUNE_ENV_WAVES 4   /* envs per env_kernel block: 1 or 4                        */
+#define FFMP_TUNE_ENV_WAVES 4   /* waves per env_kernel block: 1 or 4                       */
+#define FFMP_TUNE_ENV_LANES 5   /* lanes per env in env_kernel: 0 auto, 16, 32, 64 (>= K)   */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

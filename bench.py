@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
     p.add_argument("--frame-window", type=int, default=None,
                    help="frames per env kept in HBM (2 = contiguous (N,2,G,G) rewritten every step; default auto)")
+    p.add_argument("--ring", default="auto", choices=["auto", "seamless", "wrap"],
+                   help="frame ring with frame_window > 2: seamless (VMM alias, never wraps) or wrap")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -122,7 +124,7 @@ def cpu_baseline_parallel(cfg, seconds: float, procs: int):
                       f"1 thread per process"}
 
 
-def load_traffic(workload: str, n_envs: int, window: int):
+def load_traffic(workload: str, n_envs: int, window: int, ring: str):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if not os.path.exists(path):
@@ -130,7 +132,8 @@ def load_traffic(workload: str, n_envs: int, window: int):
     try:
         with open(path) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window:
+        if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window \
+                or d.get("ring", "wrap" if window > 2 else "contiguous") != ring:
             return None
         return float(d["raster_hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
@@ -175,7 +178,7 @@ def main():
         strong = False
     n_total = n * world
     env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
-                  frame_window=args.frame_window)
+                  frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring])
 
     K, W = args.steps, args.warmup
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -214,10 +217,11 @@ def main():
     r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * 4 * G2
     raster_ms = sum(r_ms) / len(r_ms)
     step_ms_ev = sum(a.elapsed_time(b) for a, b in evs) / K
-    b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window)
+    b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
+                           seamless=env.ring == "seamless")
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
     per_launch_envs = raster_ev[0][2]
-    traffic = load_traffic(name, per_launch_envs, env.frame_window)
+    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring)
 
     if rank == 0:
         out = {
@@ -236,7 +240,7 @@ def main():
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow),
-                       "frame_window": env.frame_window,
+                       "frame_window": env.frame_window, "ring": env.ring,
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

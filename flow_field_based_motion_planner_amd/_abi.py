@@ -110,6 +110,10 @@ _SIGS = {
     "ffmp_episode_init": (C.c_int, [_I64, _P, _I32, C.POINTER(EpisodeT), _P]),
     "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
                                       _P]),
+    "ffmp_ring_create": (C.c_int, [_I32, _I64, _I32, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
+    "ffmp_ring_destroy": (C.c_int, [_P]),
+    "ffmp_ring_pool_bytes": (_I64, [_I32]),
+    "ffmp_dlpack": (_P, [_P, _I32, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64), _I32, _P]),
 }
 
 _LIB: Optional[C.CDLL] = None
@@ -192,6 +196,60 @@ def set_tuning(key: int, value: int) -> int:
     if prev < 0:
         check(prev, "ffmp_set_tuning")
     return prev
+
+
+# ----------------------------------------------------------------- DLPack (device memory -> torch)
+# torch has no Python from_blob; libffmp builds a DLPack DLManagedTensor (with a C deleter, so
+# nothing calls back into Python when torch frees it) and the capsule hands it to torch.
+DL_CPU, DL_ROCM = 1, 10
+
+
+def tensor_from_pointer(ptr: int, shape, strides, device_type: int = DL_ROCM, device_id: int = 0,
+                        bits: int = 32, owner: Optional[int] = None):
+    """A torch float tensor over existing memory `ptr` (element strides).  `owner`: a ring
+    handle whose memory it is; the ring lives until its creator released it and every tensor
+    made from it (and every view of those) is freed."""
+    import torch.utils.dlpack as dl
+    lib = load()
+    nd = len(shape)
+    shp = (C.c_int64 * nd)(*[int(s) for s in shape])
+    std = (C.c_int64 * nd)(*[int(s) for s in strides])
+    mt = lib.ffmp_dlpack(C.c_void_p(int(ptr)), device_type, device_id, nd, shp, std, bits, owner)
+    if not mt:
+        check(-1, "ffmp_dlpack")
+    new_capsule = C.pythonapi.PyCapsule_New
+    new_capsule.restype = C.py_object
+    new_capsule.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]
+    return dl.from_dlpack(new_capsule(mt, b"dltensor", None))
+
+
+class SeamlessRing:
+    """`slots` frame planes of `slot_bytes` in device memory plus a virtual slot `slots` that is a
+    second mapping of slot 0 (include/ffmp.h ffmp_ring_create), handed to torch as ONE tensor
+    (slots + 1, *plane) with the slot stride.  The mapping is released when that tensor and
+    every view of it are freed."""
+
+    @staticmethod
+    def tensor(device_id: int, plane_shape, slots: int, bits: int = 32):
+        lib = load()
+        esize = bits // 8
+        slot_bytes = esize
+        for d in plane_shape:
+            slot_bytes *= int(d)
+        ring, base, stride = _P(), _P(), _I64()
+        check(lib.ffmp_ring_create(int(device_id), int(slot_bytes), int(slots), C.byref(ring), C.byref(base),
+                                   C.byref(stride)), "ffmp_ring_create")
+        try:
+            inner = [1]
+            for d in reversed(plane_shape[1:]):
+                inner.insert(0, inner[0] * int(d))
+            shape = (int(slots) + 1,) + tuple(int(d) for d in plane_shape)
+            strides = (stride.value // esize,) + tuple(inner)
+            t = tensor_from_pointer(base.value, shape, strides, DL_ROCM, int(device_id), bits, owner=ring.value)
+            t[:slots].zero_()  # stream-ordered with the launches that follow
+        finally:
+            lib.ffmp_ring_destroy(ring)  # the creator's reference; the tensor holds its own
+        return t, stride.value
 
 
 def footprint_from_lib(grid: int, res: float, robot_r: float):

@@ -191,11 +191,13 @@ def preset(name: str, **overrides) -> FFMPConfig:
     return FFMPConfig(**kw)
 
 
-def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True, window: int = 2) -> Dict[str, int]:
+def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True, window: int = 2,
+                       seamless: bool = False) -> Dict[str, int]:
     """Algorithmic HBM bytes of one env step.
 
     raster kernel: writes the new float32 frame of state_m (4 G^2), the older one too on the
-    steps where the frame window wraps (every W-1 steps; every step for W = 2) — plus, not
+    steps where the frame window wraps (every W-1 steps; every step for W = 2; never with the
+    seamless ring) — plus, not
     counted here, the older frame of each env reset on the other steps —, the float32 potential
     plane (4 G^2) and, with cfg.flow, the two float32 flow planes (8 G^2); reads the raster
     record (64 + 48 K).  state kernel: reads/writes pose, goal, d0, t, episode, obstacles and
@@ -204,7 +206,7 @@ def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True, window: int = 2)
     G2 = cfg.grid * cfg.grid
     K, L = cfg.n_obst, cfg.n_beams
     rec = 4 * cfg.record_len()
-    frames = 4 * G2 + (4 * G2) // (max(int(window), 2) - 1)
+    frames = 4 * G2 + (0 if seamless and window > 2 else (4 * G2) // (max(int(window), 2) - 1))
     raster = frames + (4 * G2 if potential else 0) + (8 * G2 if cfg.flow else 0) + rec
     state_rw = 2 * (24 + 16 + 8 + 4 + 4 + 40 * K)  # pose, goal, d0, t, episode, obst(32)+r(8)
     small_obs = 4 * (2 + 2 + 1 + 2) + 4 * L + rec + 8 + 4 + 4  # g, v, t, grad, lidar, record, action, reward, flags

@@ -19,6 +19,9 @@
 #include <stddef.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "ffmp_device.h"
 
 #pragma clang fp contract(off)
@@ -993,6 +996,218 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
   hipLaunchKernelGGL(episode_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      n, *out, window, max_steps, threshold, flags, *ep);
   return check_launch("ffmp_episode_update");
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ seamless frame ring
+// Physical: slot 0 (its own handle, so it can be mapped twice with offset 0 — hipMemMap's
+// offset must be 0) and slots 1..W-1 (one handle).  Virtual: [slot 0 | slots 1..W-1 | slot 0].
+//
+// Rings are never unmapped while the process runs.  On ROCm 7.x, once a VMM range has been
+// unmapped and its address freed, a later mapping at a reused address is not reliably what the
+// runtime resolves: a kernel whose pointer argument falls in the reused range, or a copy from
+// it, can reach the OLD allocation (tools/ring_reuse_probe.hip: D2H copies of a fresh mapping
+// return the previous ring's bytes, with or without the alias; FFMPVec saw the first raster
+// into a fresh ring vanish).  So a destroyed ring — the last reference dropped — is parked in
+// a process-wide pool and handed out again to the next ring of the same device and slot count
+// whose slots fit its stride; nothing is ever returned to the driver before exit.
+struct ffmp_ring {
+  int32_t device;
+  int32_t slots;
+  size_t stride;
+  char* va;
+  size_t vbytes;
+  hipMemGenericAllocationHandle_t h0, h1;
+  int mapped;  // bit 0: slot 0, bit 1: slots 1..W-1, bit 2: the alias
+  int refs;    // the creator + one per live DLPack tensor (atomic); 0 = parked in the pool
+};
+
+// dlpack.h (v0.8) DLManagedTensor, the interchange torch.utils.dlpack.from_dlpack consumes
+struct DLDevice_ { int32_t device_type, device_id; };
+struct DLDataType_ { uint8_t code, bits; uint16_t lanes; };
+struct DLTensor_ {
+  void* data;
+  DLDevice_ device;
+  int32_t ndim;
+  DLDataType_ dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor_ {
+  DLTensor_ dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor_*);
+};
+struct DLHolder_ {  // one allocation: the managed tensor, its shape/strides, its owner
+  DLManagedTensor_ mt;
+  int64_t dims[16];
+  ffmp_ring* owner;
+};
+
+namespace {
+
+std::mutex g_pool_mu;
+std::vector<ffmp_ring*> g_pool;  // parked rings (refs == 0), mapped, reusable
+
+// Only for a ring whose creation failed half-way (never used by a launch): unmap what was
+// mapped and give it back.
+void ring_undo(ffmp_ring* r) {
+  if (r->mapped & 4) (void)hipMemUnmap(r->va + r->stride * r->slots, r->stride);
+  if (r->mapped & 2) (void)hipMemUnmap(r->va + r->stride, r->stride * (r->slots - 1));
+  if (r->mapped & 1) (void)hipMemUnmap(r->va, r->stride);
+  if (r->va) (void)hipMemAddressFree(r->va, r->vbytes);
+  if (r->h1) (void)hipMemRelease(r->h1);
+  if (r->h0) (void)hipMemRelease(r->h0);
+  delete r;
+}
+
+void ring_unref(ffmp_ring* r) {
+  if (__atomic_sub_fetch(&r->refs, 1, __ATOMIC_ACQ_REL) > 0) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.push_back(r);
+}
+
+// restores the caller's current device on scope exit
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, ffmp_ring_t** ring, void** base,
+                     int64_t* slot_stride) {
+  if (!ring || !base || !slot_stride) return fail(FFMP_E_ARG, "ffmp_ring_create: NULL output pointer");
+  *ring = nullptr;
+  *base = nullptr;
+  if (slot_bytes <= 0 || slots < 2) return fail(FFMP_E_ARG, "ffmp_ring_create: slot_bytes > 0 and slots >= 2 required");
+  {  // a parked ring of this shape: the tightest fit
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    size_t best = (size_t)-1, at = 0;
+    for (size_t k = 0; k < g_pool.size(); ++k) {
+      const ffmp_ring* p = g_pool[k];
+      if (p->device == device && p->slots == slots && p->stride >= (size_t)slot_bytes && p->stride < best &&
+          p->stride <= 2 * (size_t)slot_bytes + (2u << 20)) {
+        best = p->stride;
+        at = k;
+      }
+    }
+    if (best != (size_t)-1) {
+      ffmp_ring* r = g_pool[at];
+      g_pool.erase(g_pool.begin() + at);
+      r->refs = 1;
+      *ring = r;
+      *base = r->va;
+      *slot_stride = (int64_t)r->stride;
+      return FFMP_OK;
+    }
+  }
+  DeviceScope scope(device);
+  int vmm = 0;
+  if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
+    return fail(FFMP_E_HIP, "ffmp_ring_create: device %d has no virtual memory management", device);
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
+  if (e != hipSuccess || gran == 0) return fail(FFMP_E_HIP, "hipMemGetAllocationGranularity: %s", hipGetErrorString(e));
+  ffmp_ring* r = new ffmp_ring();
+  r->device = device;
+  r->slots = slots;
+  r->stride = ((size_t)slot_bytes + gran - 1) / gran * gran;
+  r->vbytes = r->stride * (size_t)(slots + 1);
+  const char* what = "hipMemCreate";
+  if ((e = hipMemCreate(&r->h0, r->stride, &prop, 0)) != hipSuccess) goto fail_;
+  if ((e = hipMemCreate(&r->h1, r->stride * (size_t)(slots - 1), &prop, 0)) != hipSuccess) goto fail_;
+  what = "hipMemAddressReserve";
+  if ((e = hipMemAddressReserve((void**)&r->va, r->vbytes, gran, nullptr, 0)) != hipSuccess) {
+    r->va = nullptr;
+    goto fail_;
+  }
+  what = "hipMemMap";
+  if ((e = hipMemMap(r->va, r->stride, 0, r->h0, 0)) != hipSuccess) goto fail_;
+  r->mapped |= 1;
+  if ((e = hipMemMap(r->va + r->stride, r->stride * (size_t)(slots - 1), 0, r->h1, 0)) != hipSuccess) goto fail_;
+  r->mapped |= 2;
+  what = "hipMemMap (alias of slot 0)";
+  if ((e = hipMemMap(r->va + r->stride * (size_t)slots, r->stride, 0, r->h0, 0)) != hipSuccess) goto fail_;
+  r->mapped |= 4;
+  {
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    what = "hipMemSetAccess";
+    if ((e = hipMemSetAccess(r->va, r->vbytes, &acc, 1)) != hipSuccess) goto fail_;
+  }
+  r->refs = 1;
+  *ring = r;
+  *base = r->va;
+  *slot_stride = (int64_t)r->stride;
+  return FFMP_OK;
+fail_:
+  fail(FFMP_E_HIP, "ffmp_ring_create: %s: %s", what, hipGetErrorString(e));
+  (void)hipGetLastError();
+  ring_undo(r);
+  return FFMP_E_HIP;
+}
+
+int ffmp_ring_destroy(ffmp_ring_t* ring) {
+  if (ring) ring_unref(ring);
+  return FFMP_OK;
+}
+
+int64_t ffmp_ring_pool_bytes(int32_t device) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int64_t b = 0;
+  for (const ffmp_ring* p : g_pool)
+    if (p->device == device || device < 0) b += (int64_t)(p->stride * (size_t)p->slots);
+  return b;
+}
+
+static void dl_delete(DLManagedTensor_* mt) {
+  DLHolder_* h = (DLHolder_*)mt->manager_ctx;
+  if (h->owner) ring_unref(h->owner);
+  free(h);
+}
+
+void* ffmp_dlpack(void* data, int32_t device_type, int32_t device_id, int32_t ndim, const int64_t* shape,
+                  const int64_t* strides, int32_t bits, ffmp_ring_t* owner) {
+  if (!data || ndim < 1 || ndim > 8 || !shape || !strides || (bits != 8 && bits != 16 && bits != 32 && bits != 64)) {
+    fail(FFMP_E_ARG, "ffmp_dlpack: bad arguments");
+    return nullptr;
+  }
+  DLHolder_* h = (DLHolder_*)calloc(1, sizeof(DLHolder_));
+  if (!h) {
+    fail(FFMP_E_ARG, "ffmp_dlpack: out of host memory");
+    return nullptr;
+  }
+  for (int d = 0; d < ndim; ++d) {
+    h->dims[d] = shape[d];
+    h->dims[8 + d] = strides[d];
+  }
+  h->mt.dl_tensor.data = data;
+  h->mt.dl_tensor.device = {device_type, device_id};
+  h->mt.dl_tensor.ndim = ndim;
+  h->mt.dl_tensor.dtype = {2 /* kDLFloat */, (uint8_t)bits, 1};
+  h->mt.dl_tensor.shape = h->dims;
+  h->mt.dl_tensor.strides = h->dims + 8;
+  h->mt.manager_ctx = h;
+  h->mt.deleter = dl_delete;
+  h->owner = owner;
+  if (owner) __atomic_add_fetch(&owner->refs, 1, __ATOMIC_ACQ_REL);
+  return &h->mt;
 }
 
 }  // extern "C"

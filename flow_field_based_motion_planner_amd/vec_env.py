@@ -59,13 +59,18 @@ class FFMPVec:
             contiguous plane per slot.  Every W-1 steps the pair wraps to slot 0 (both frames
             written).  W = 2: the contiguous (N,2,G,G) layout, both frames written every step.
             None: 8 for large batches when HBM allows, else 2.
+        seamless: W > 2 only.  True: the ring is HIP virtual memory with one extra virtual slot
+            mapped onto slot 0's pages (include/ffmp.h ffmp_ring_create), so the pair never
+            wraps and every step writes only the new frame; `frames` is (W+1, N, G, G) with
+            frames[W] aliasing frames[0].  None (default): seamless when the device supports
+            it, else the wrapping ring.  False: always the wrapping ring.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
-                 frame_window: Optional[int] = None):
+                 frame_window: Optional[int] = None, seamless: Optional[bool] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -90,6 +95,10 @@ class FFMPVec:
         self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
         self.raster_shape_newest = (0, 0)  # the same for newest-only launches (frame ring)
         self.frame_window = self._pick_window(frame_window)
+        self._seamless_req = seamless if self.frame_window > 2 else False
+        if seamless and self.frame_window == 2:
+            raise ValueError("seamless=True needs frame_window > 2")
+        self.ring = "contiguous" if self.frame_window == 2 else "wrap"  # or "seamless" (set by _alloc)
         self._wpos = 0  # frame slot of state_m[:, 0]
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
@@ -126,7 +135,7 @@ class FFMPVec:
         budget = self.WINDOW_HBM_FRACTION * free - other
         return int(max(2, min(self.WINDOW_DEFAULT, budget // plane)))
 
-    def _buffer_specs(self):
+    def _buffer_specs(self, with_frames: bool = True):
         """(name, shape, dtype) of every per-shard device buffer."""
         cfg, N = self.cfg, self.num_envs
         G, K, L = cfg.grid, cfg.n_obst, cfg.n_beams
@@ -157,13 +166,39 @@ class FFMPVec:
             specs = [sp for sp in specs if sp[0] != "lidar"]
         if not self.keep_terminal:
             specs = [sp for sp in specs if not sp[0].startswith("term_")]
+        if not with_frames:
+            specs = [sp for sp in specs if sp[0] != "frames"]
         return specs
 
-    def _alloc(self):
+    def _alloc_ring(self) -> bool:
+        """The seamless frame ring (HIP VMM, virtual slot W aliasing slot 0), if requested and
+        the device supports it."""
+        self._ring_stride = None
+        if self._seamless_req is False:
+            return False
+        N, G = self.num_envs, self.cfg.grid
+        try:
+            self.frames, stride = _abi.SeamlessRing.tensor(self.device.index, (N, G, G), self.frame_window)
+        except _abi.FFMPBackendError:
+            if self._seamless_req:
+                raise
+            self._seamless_req = False  # no VMM here: the wrapping ring from now on
+            return False
+        self._ring_stride = stride
+        self.ring = "seamless"
+        return True
+
+    def _alloc(self, keep_ring: bool = False):
         """All per-shard buffers, zero-initialised.  With arena=True (default) they are views
-        into ONE device allocation carved at 2 MiB boundaries, planes first."""
+        into ONE device allocation carved at 2 MiB boundaries, planes first (the seamless frame
+        ring, when used, is its own VMM mapping; keep_ring: re-allocate everything else)."""
         dev = self.device
-        specs = self._buffer_specs()
+        if keep_ring and self.ring == "seamless":
+            seamless = True
+        else:
+            self.frames = None
+            seamless = self._alloc_ring()
+        specs = self._buffer_specs(with_frames=not seamless)
         self.potential = None
         self.lidar = None
         self.flow = None
@@ -196,7 +231,7 @@ class FFMPVec:
     def _carve(self, base: int) -> None:
         """Point every buffer into the arena, starting `base` bytes in."""
         self._arena_base = base
-        for (name, shape, dtype), o in zip(self._buffer_specs(), self._arena_offs):
+        for (name, shape, dtype), o in zip(self._buffer_specs(with_frames=self.ring != "seamless"), self._arena_offs):
             nb = self._nbytes(shape, dtype)
             setattr(self, name, self._arena_buf[base + o:base + o + nb].view(dtype).view(shape))
 
@@ -250,9 +285,9 @@ class FFMPVec:
     PLACEMENT_SPACER = 1 << 30
 
     def _retry_placement(self) -> None:
-        names = [n for n, _, _ in self._buffer_specs()]
+        names = [n for n, _, _ in self._buffer_specs()]  # includes "frames" (arena or ring)
         keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
-                 (self.raster_shape, self.raster_shape_newest), self.placement)]
+                 (self.raster_shape, self.raster_shape_newest), self.placement, self._ring_stride)]
         spacers = []
         tries = [round(self.placement["gbs"], 1)]
         for k in range(self.PLACEMENT_RETRIES):
@@ -262,14 +297,14 @@ class FFMPVec:
             if free < 1.2 * self._arena_buf.numel() + (k + 1) * self.PLACEMENT_SPACER + (1 << 30):
                 break
             spacers.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
-            self._alloc()
+            self._alloc(keep_ring=True)  # a seamless ring is kept (rings are never unmapped)
             self._build_structs()
             self._autotune_raster()
             tries.append(round(self.placement["gbs"], 1))
             keep.append((self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
-                         (self.raster_shape, self.raster_shape_newest), self.placement))
+                         (self.raster_shape, self.raster_shape_newest), self.placement, self._ring_stride))
         best = max(range(len(keep)), key=lambda i: keep[i][0])
-        _, buf, views, shapes, placement = keep[best]
+        _, buf, views, shapes, placement, self._ring_stride = keep[best]
         self._arena_buf = buf
         for n, v in views.items():
             setattr(self, n, v)
@@ -284,7 +319,7 @@ class FFMPVec:
         results = []
         plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) + (1.0 if self.flow is not None else 0.0))
         steps = 3 if plane_bytes >= (8 << 30) else 12  # >= ~10 ms of timed raster per shape
-        cyc = self.frame_window - 1  # whole window cycles: one full raster + W-2 newest-only
+        cyc = self.frame_window - 1 if self.ring == "wrap" else 1  # whole cycles of the wrapping ring
         steps = -(-steps // cyc) * cyc
         for shape in self.RASTER_SHAPES:
             self.raster_shape = self.raster_shape_newest = shape
@@ -294,12 +329,19 @@ class FFMPVec:
             got = [(r[kind][0], r[kind][1], shape) for r, shape in results if kind in r]
             if got:
                 best[kind] = max(got)
-        self.raster_shape = best[True][2]
+        if True in best:
+            self.raster_shape = best[True][2]
+        else:  # seamless ring: steps never write both frames; resets use the newest-only winner
+            self.raster_shape = best[False][2]
         self.raster_shape_newest = best[False][2] if False in best else self.raster_shape
         # the cycle's bandwidth with the chosen shapes: one full launch + W-2 newest-only ones
+        # (the wrapping ring), only full launches (W = 2) or only newest-only ones (seamless)
         n_new = self.frame_window - 2
-        b = self._raster_bytes(self.num_envs, True) + n_new * self._raster_bytes(self.num_envs, False)
-        ms = best[True][1] + (n_new * best[False][1] if n_new else 0.0)
+        n_full = 1
+        if self.ring == "seamless":
+            n_new, n_full = 1, 0
+        b = n_full * self._raster_bytes(self.num_envs, True) + n_new * self._raster_bytes(self.num_envs, False)
+        ms = (best[True][1] if n_full else 0.0) + (n_new * best[False][1] if n_new else 0.0)
         gbs = b / (ms * 1e-3) / 1e9
         self.placement = {"shape": {"cells_per_block": self.raster_shape[0], "flags": self.raster_shape[1]},
                           "shape_newest": ({"cells_per_block": self.raster_shape_newest[0],
@@ -309,6 +351,8 @@ class FFMPVec:
                                          for r, (c, f) in results]}
         if self._arena_buf is not None:
             self._arena_buf.zero_()
+        if self.ring == "seamless":
+            self.frames[:self.frame_window].zero_()
         self._needs_reset = True
 
     def _build_structs(self):
@@ -368,12 +412,13 @@ class FFMPVec:
     def _sm_strides(self):
         """(env stride, frame stride) of state_m in floats, for ffmp_obs_t."""
         G2 = self.cfg.grid * self.cfg.grid
-        return (2 * G2, G2) if self.frame_window == 2 else (G2, self.num_envs * G2)
+        if self.frame_window == 2:
+            return (2 * G2, G2)
+        return (G2, self.frames.stride(0))
 
     def _set_window(self, p: int) -> None:
         self._wpos = p
-        slot = self.num_envs * self.cfg.grid * self.cfg.grid * 4
-        self._obs_c.state_m = self.frames.data_ptr() + p * slot
+        self._obs_c.state_m = self.frames.data_ptr() + p * self.frames.stride(0) * 4
 
     def _raster_bytes(self, n: int, full: bool) -> int:
         """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs
@@ -460,7 +505,11 @@ class FFMPVec:
         """Kernel 2 of a step (the HBM-bound hot kernel): slide the frame pair by one and raster
         the new frame + potential (+ flow), or both frames when the window wraps or W == 2."""
         p = self._wpos + 1
-        full = p > self.frame_window - 2
+        if self.ring == "seamless":  # virtual slot W is slot 0: the pair slides forever
+            full = False
+            p %= self.frame_window
+        else:
+            full = p > self.frame_window - 2
         self._set_window(0 if full else p)
         self._raster_launch(full, None, timing)
 
@@ -574,6 +623,7 @@ class FFMPVec:
     def close(self) -> None:
         """Release the device buffers (the object is unusable afterwards)."""
         self._needs_reset = True
+        torch.cuda.synchronize(self.device)
         for name, _, _ in self._buffer_specs():
             setattr(self, name, None)
         self._arena_buf = None
@@ -606,14 +656,15 @@ class FFMPVec:
 
     def hbm_bytes(self) -> int:
         if self._arena_buf is not None:
-            return self._arena_buf.numel()
+            ring = self.frame_window * self.frames.stride(0) * 4 if self.ring == "seamless" else 0
+            return self._arena_buf.numel() + ring
         return sum(t.numel() * t.element_size() for t in vars(self).values() if isinstance(t, torch.Tensor))
 
     def __repr__(self):
         c = self.cfg
         return (f"FFMPVec(num_envs={self.num_envs}, G={c.grid}, K={c.n_obst}, L={c.n_beams}, "
                 f"moving={c.moving}, device={self.device}, env_offset={self.env_offset}, "
-                f"frame_window={self.frame_window})")
+                f"frame_window={self.frame_window}, ring={self.ring})")
 
 
 __all__ = ["FFMPVec", "PRESETS"]

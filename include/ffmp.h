@@ -3,8 +3,9 @@
  * motion-planning environment (the `gym_ffmp` step/reset hot path).
  *
  * Every buffer is caller-owned, contiguous, env-major DEVICE memory (in
- * practice torch tensors' data_ptr()).  Nothing here allocates, prints or
- * throws.  Each call enqueues work on `stream` (a hipStream_t passed as void*;
+ * practice torch tensors' data_ptr()).  Nothing here allocates (except the
+ * optional frame-ring helper ffmp_ring_create at the end), prints or throws.
+ * Each call enqueues work on `stream` (a hipStream_t passed as void*;
  * NULL = the legacy default stream) and returns 0, or a negative FFMP_E_* code
  * with a message readable from ffmp_last_error() (thread-local).
  *
@@ -277,6 +278,38 @@ int ffmp_episode_init(int64_t n, const uint8_t* mask, int32_t flags, ffmp_episod
  * out.truncated; reward unused).  max_steps = 0 when out.done already includes truncation. */
 int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps,
                         double threshold, int32_t flags, ffmp_episode_t* ep, void* stream);
+
+/* Seamless frame ring — an optional allocation helper (the step / raster entry points above
+ * still never allocate).  The temporal stack of make_temporal_maps (src/train.py:474-486)
+ * keeps the previous frame beside the new one; kept in place as a ring of `slots` frame
+ * planes, the [older, newest] pair is the view of two consecutive slots [p, p+1].  A plain
+ * array has no slot after the last one, so such a ring must wrap (and rewrite both frames)
+ * every slots-1 steps.  This ring reserves (slots + 1) * slot_stride bytes of virtual address
+ * space over `slots` physical slots of `device` (HIP virtual memory management) and maps
+ * virtual slot `slots` onto the physical pages of slot 0 a second time, so the pair [p, p+1]
+ * exists for every p in [0, slots): the view slides by one slot per step forever.
+ *   slot_stride = slot_bytes rounded up to the allocation granularity (out);
+ *   *base = the first virtual slot (device pointer); contents undefined (zero them on the
+ *   stream that will use them).
+ * Returns 0, FFMP_E_ARG, or FFMP_E_HIP (no VMM support, out of memory, ...; then use a plain
+ * ring — ffmp_last_error() says which call failed).
+ * ffmp_ring_destroy drops the creator's reference.  A ring is never unmapped while the process
+ * runs (ROCm 7 can resolve a reused, re-mapped VMM address to the old allocation — see
+ * ffmp_kernels.hip); once its last reference is gone it is parked and handed out again by the
+ * next ffmp_ring_create of the same device and slot count whose slots fit its stride (up to
+ * 2x + 2 MiB).  ffmp_ring_pool_bytes: physical bytes parked (device < 0: all devices). */
+typedef struct ffmp_ring ffmp_ring_t;
+int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, ffmp_ring_t** ring,
+                     void** base, int64_t* slot_stride);
+int ffmp_ring_destroy(ffmp_ring_t* ring);
+int64_t ffmp_ring_pool_bytes(int32_t device);
+/* A dlpack.h (v0.8) DLManagedTensor* of float `bits` elements over `data` (element strides,
+ * ndim <= 8), for consumers that take DLPack (torch.utils.dlpack.from_dlpack, CuPy, JAX).
+ * Its deleter frees it and, when `owner` is a ring, drops the reference it took on it: a ring
+ * is parked once ffmp_ring_destroy was called AND every such tensor was deleted.
+ * NULL on bad arguments. */
+void* ffmp_dlpack(void* data, int32_t device_type, int32_t device_id, int32_t ndim, const int64_t* shape,
+                  const int64_t* strides, int32_t bits, ffmp_ring_t* owner);
 
 #ifdef __cplusplus
 }

@@ -265,15 +265,21 @@ def test_autotune_picks_a_candidate():
     env.step(torch.zeros(8192, dtype=torch.int64, device="cuda:0"))
 
 
+@pytest.mark.parametrize("ring", ["seamless", "wrap"])
 @pytest.mark.parametrize("window", [3, 4, 8])
-def test_frame_window_equals_contiguous(window):
-    """The in-place temporal stack (frame window W, newest-only rasters + wraps) yields the same
+def test_frame_window_equals_contiguous(window, ring):
+    """The in-place temporal stack (frame window W: newest-only rasters, plus wraps for the
+    wrapping ring; the seamless ring's virtual slot W is slot 0 again) yields the same
     observations, bit for bit, as rewriting both frames every step (W = 2), across resets."""
     cfg = FFMPConfig(grid=64, n_obst=24, n_beams=16, moving=True, obst_rmax=0.6, obst_vmax=1.5, world_half=3.0,
                      max_steps=7, flow=True, seed=41)
     n = 40
     a = FFMPVec(n, cfg, device="cuda:0", frame_window=2)
-    b = FFMPVec(n, cfg, device="cuda:0", frame_window=window)
+    b = FFMPVec(n, cfg, device="cuda:0", frame_window=window, seamless=ring == "seamless")
+    assert b.ring == ring and a.ring == "contiguous"
+    if ring == "seamless":  # slot W is a second mapping of slot 0 (padded slot stride)
+        assert b.frames.shape[0] == window + 1 and b.frames.stride(0) >= n * 64 * 64
+        assert b.frames[window].data_ptr() != b.frames[0].data_ptr()
     assert not b.state_m.is_contiguous() and b.state_m.shape == a.state_m.shape
     a.reset()
     b.reset()
@@ -295,6 +301,11 @@ def test_frame_window_equals_contiguous(window):
             b.reset(mask=m)
             assert torch.equal(a.state_m, b.state_m)
     assert resets > 0
+    if ring == "seamless":
+        assert torch.equal(b.frames[window], b.frames[0])
+        b.frames[window, 3, 5, 7] = 17.0  # a write through the alias is seen through slot 0
+        torch.cuda.synchronize()
+        assert float(b.frames[0, 3, 5, 7]) == 17.0
     sd = b.state_dict()  # checkpoint round trip re-rasters the current pair in place
     b.state_m.fill_(-1.0)
     b.load_state_dict(sd)

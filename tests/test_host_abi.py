@@ -130,6 +130,9 @@ def test_bytes_model():
     # frame window W: the older frame is written on 1 step in W-1 (plus resets, counted by bench.py)
     assert bytes_per_env_step(preset("C3"), window=8)["raster"] == 8 * 65536 + (4 * 65536) // 7 + 4 * (16 + 12 * 16)
     assert bytes_per_env_step(preset("C3"), window=2)["raster"] == b["raster"]
+    # seamless ring: never wraps, only the new frame (plus resets)
+    assert bytes_per_env_step(preset("C3"), window=8, seamless=True)["raster"] == 8 * 65536 + 4 * (16 + 12 * 16)
+    assert bytes_per_env_step(preset("C3"), window=2, seamless=True)["raster"] == b["raster"]
     assert b["total"] > b["raster"]
 
 
@@ -162,3 +165,35 @@ def test_episode_abi_validation_no_gpu(lib):
     assert lib.ffmp_episode_init(4, None, 0, C.byref(bad), None) == -1
     assert lib.ffmp_episode_update(0, C.byref(out), 10, 0, 0.8, 1, C.byref(ep), None) == 0
     assert lib.ffmp_episode_init(-1, None, 0, C.byref(ep), None) == -1
+
+
+def test_dlpack_view_over_host_memory(lib):
+    """ffmp_dlpack + the capsule hand-off (how the seamless ring reaches torch), exercised on
+    host memory: shape, element strides (incl. a padded slot stride), aliasing, lifetime."""
+    import gc
+
+    import torch
+
+    from flow_field_based_motion_planner_amd import _abi
+    a = np.arange(3 * 20, dtype=np.float32)
+    t = _abi.tensor_from_pointer(a.ctypes.data, (3, 2, 4), (20, 4, 1), _abi.DL_CPU, 0)
+    assert t.shape == (3, 2, 4) and t.stride() == (20, 4, 1) and t.dtype == torch.float32
+    assert float(t[2, 1, 3]) == a[2 * 20 + 1 * 4 + 3]
+    v = t[1:3].transpose(0, 1)  # the state_m-style pair view
+    del t
+    gc.collect()
+    a[20] = -5.0  # a view, not a copy
+    assert float(v[0, 0, 0]) == -5.0
+    assert not lib.ffmp_dlpack(None, 1, 0, 1, None, None, 32, None)  # bad arguments -> NULL
+
+
+def test_ring_api_without_gpu(lib):
+    """The ring helper validates its arguments and, without a GPU, fails with a message."""
+    import ctypes as C
+    ring, base, stride = C.c_void_p(), C.c_void_p(), C.c_int64()
+    assert lib.ffmp_ring_create(0, 0, 4, C.byref(ring), C.byref(base), C.byref(stride)) == -1
+    assert lib.ffmp_ring_create(0, 4096, 1, C.byref(ring), C.byref(base), C.byref(stride)) == -1
+    rc = lib.ffmp_ring_create(0, 1 << 20, 4, C.byref(ring), C.byref(base), C.byref(stride))
+    assert rc == -2 and not ring.value and b"ffmp_ring_create" in lib.ffmp_last_error()
+    assert lib.ffmp_ring_destroy(None) == 0
+    assert lib.ffmp_ring_pool_bytes(-1) == 0

@@ -89,12 +89,14 @@ def main():
         alg = bj["roofline"]["algorithmic_bytes_per_launch"]
         pm["n_envs"] = n
         pm["frame_window"] = bj["config"].get("frame_window", 2)
+        pm["ring"] = bj["config"].get("ring", "wrap" if pm["frame_window"] > 2 else "contiguous")
         pm["raster_algorithmic_bytes_per_launch"] = alg
         if "raster_kernel" in pm["kernels"]:
             hb = pm["kernels"]["raster_kernel"]["hbm_bytes"]
             pm["raster_traffic_over_algorithmic"] = hb / alg
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
-                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "raster_hbm_bytes_per_launch": hb,
+                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"],
+                           "raster_hbm_bytes_per_launch": hb,
                            "source": f"{tag}_{cfg}_pmc.json"}, f, indent=1)
     trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")
     if trace and bj:

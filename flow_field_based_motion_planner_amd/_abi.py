@@ -188,6 +188,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
 
 TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES, TUNE_ENV_LANES = 1, 2, 3, 4, 5
 RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
+RASTER_TILE2, RASTER_TILE4, RASTER_TILE8 = 16, 32, 64
 
 
 def set_tuning(key: int, value: int) -> int:

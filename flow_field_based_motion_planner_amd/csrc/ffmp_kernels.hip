@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
                                                      float* __restrict__ state_m, int64_t sm_stride,
                                                      int64_t sm_frame, int32_t newest_only,
                                                      float* __restrict__ pot,
-                                                     float* __restrict__ flow) {
+                                                     float* __restrict__ flow, int32_t tile_log2r) {
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
   __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
   __shared__ float s_hdr[FFMP_REC_HDR];
@@ -476,14 +476,9 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const int qbeg = tile * cells_per_block;
   const int qend = min(qbeg + cells_per_block, G2);
 
-  for (int q0 = qbeg + wave * 256; q0 < qend; q0 += 1024) {
-    // ---- wave chunk [q0, qlast] -> ego bounding box (wave-uniform) ----
-    const int qlast = min(q0 + 255, G2 - 1);
-    const int i0 = q0 / G;
-    const int r0 = q0 - i0 * G;
-    const int i1 = i0 + small_div(r0 + (qlast - q0), invG);
-    int j0 = 0, j1 = G - 1;
-    if (i0 == i1) { j0 = r0; j1 = r0 + (qlast - q0); }
+  // One wave task: the cells of ego rows [i0, i1] x columns [j0, j1] (the cull box), this
+  // lane's 4 cells (i, j..j+3) at plane offset q, `valid` = the lane has cells.
+  auto task = [&](int i0, int i1, int j0, int j1, int i, int j, int q, bool valid) {
     const float bx0 = (float)i0 * res - half, bx1 = (float)i1 * res - half;
     const float by0 = (float)j0 * res - half, by1 = (float)j1 * res - half;
 
@@ -494,14 +489,9 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
                                                              (lane & 2) ? by1 : by0));
     const bool walls_c = (wb & 0xFull) != 0xFull;
     const bool walls_p = write_old && (wb & 0xF0ull) != 0xF0ull;
+    if (!valid) return;
 
     // ---- this lane's 4 cells ----
-    const int off = r0 + lane * 4;
-    const int q = q0 + lane * 4;
-    if (q >= qend) continue;
-    const int di = small_div(off, invG);
-    const int i = i0 + di;
-    const int j = off - di * G;
     const float ex = (float)i * res - half;
     float ey[4];
 #pragma unroll
@@ -542,6 +532,42 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
     if (FLOW) {
       store4<NT>(f0 + q, fx[0], fx[1], fx[2], fx[3]);
       store4<NT>(f0 + G2 + q, fy[0], fy[1], fy[2], fy[3]);
+    }
+  };
+
+  if (tile_log2r > 0) {
+    // 2-D wave tiles of R rows x C = 256/R columns (the host checked G % C == 0 and that the
+    // block holds whole bands of R rows): a compact cull box (C3, R = 4: 0.2 m x 3.2 m instead
+    // of one 12.8 m row), so far fewer discs survive the cull; every row segment is C*4 bytes
+    // of contiguous, 16-B-per-lane stores.  Tiles are dealt band-major to the 4 waves, so the
+    // waves of a block write neighbouring columns of the same rows at once.
+    const int R = 1 << tile_log2r, C = 256 >> tile_log2r;
+    const int lanes_per_row = 64 >> tile_log2r;
+    const int ncb = G / C;
+    const int row0 = qbeg / G;
+    const int ntiles = ((qend - qbeg) / G / R) * ncb;
+    const int r = lane / lanes_per_row;
+    const int c4 = (lane - r * lanes_per_row) * 4;
+    for (int t = wave; t < ntiles; t += 4) {
+      const int band = t / ncb;
+      const int cb = t - band * ncb;
+      const int i0 = row0 + band * R, j0 = cb * C;
+      const int i = i0 + r, j = j0 + c4;
+      task(i0, i0 + R - 1, j0, j0 + C - 1, i, j, i * G + j, true);
+    }
+  } else {
+    for (int q0 = qbeg + wave * 256; q0 < qend; q0 += 1024) {
+      // ---- wave chunk [q0, qlast] (256 consecutive cells) -> ego bounding box ----
+      const int qlast = min(q0 + 255, G2 - 1);
+      const int i0 = q0 / G;
+      const int r0 = q0 - i0 * G;
+      const int i1 = i0 + small_div(r0 + (qlast - q0), invG);
+      int j0 = 0, j1 = G - 1;
+      if (i0 == i1) { j0 = r0; j1 = r0 + (qlast - q0); }
+      const int off = r0 + lane * 4;
+      const int q = q0 + lane * 4;
+      const int di = small_div(off, invG);
+      task(i0, i1, j0, j1, i0 + di, off - di * G, q, q < qend);
     }
   }
 }
@@ -897,11 +923,18 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
     return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld floats (G*G = %d)",
                 (long long)sm_stride, (long long)sm_frame, G2);
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
+  // 2-D wave tiles: R rows x 256/R columns, where the plane and the block split into them
+  int32_t tile_log2r = (flags & FFMP_RASTER_TILE8) ? 3 : (flags & FFMP_RASTER_TILE4) ? 2 : (flags & FFMP_RASTER_TILE2) ? 1 : 0;
+  if (tile_log2r) {
+    const int C = 256 >> tile_log2r, R = 1 << tile_log2r;
+    const bool whole_bands = cpb >= G2 || (cpb % (cfg->grid * R)) == 0;
+    if ((cfg->grid % C) != 0 || !whole_bands) tile_log2r = 0;  // the 1-D chunks (identical results)
+  }
   const dim3 grid((unsigned)blocks), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define FFMP_RASTER_LAUNCH(NT_, XCD_, FL_)                                                              \
   hipLaunchKernelGGL((raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, \
-                     obs->state_m, sm_stride, sm_frame, newest, obs->potential, obs->flow)
+                     obs->state_m, sm_stride, sm_frame, newest, obs->potential, obs->flow, tile_log2r)
   const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
   switch (sel) {
     case 0: FFMP_RASTER_LAUNCH(false, false, false); break;

@@ -205,6 +205,11 @@ int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                                 (reset: older == newest); the caller points state_m one frame past
                                 the previous call's older slot, so [:,0] already holds the previous
                                 newest frame */
+#define FFMP_RASTER_TILE2 16 /* wave task = a 2 x 128-cell tile instead of 256 consecutive cells */
+#define FFMP_RASTER_TILE4 32 /* 4 x 64-cell tile (compact cull box: fewer discs per task)       */
+#define FFMP_RASTER_TILE8 64 /* 8 x 32-cell tile; any TILE flag needs G % (256/R) == 0 and blocks
+                                of whole R-row bands (cells_per_block % (G*R) == 0 or >= G*G),
+                                else the 256-cell chunks are used */
 int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                    const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
                    int32_t flags, void* stream);

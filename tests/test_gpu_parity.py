@@ -223,7 +223,9 @@ def test_raster_shapes_identical():
     env.reset()
     env.step(torch.randint(0, 28, (37,), device="cuda:0"))
     ref = None
-    for shape in FFMPVec.RASTER_SHAPES + ((1024, 0), (3072, _abi.RASTER_XCD), (8192, 0)):
+    extra = ((1024, 0), (3072, _abi.RASTER_XCD), (8192, 0), (1024, _abi.RASTER_TILE4),
+             (3072, _abi.RASTER_TILE8 | _abi.RASTER_XCD), (2048, _abi.RASTER_TILE2), (1024, _abi.RASTER_TILE8))
+    for shape in FFMPVec.RASTER_SHAPES + extra:
         env.state_m.fill_(-1.0)
         env.potential.fill_(-1.0)
         env.raster_shape = shape
@@ -232,6 +234,33 @@ def test_raster_shapes_identical():
         if ref is None:
             ref = got
         assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), shape
+
+
+@pytest.mark.parametrize("grid", [256, 96, 100])
+def test_tile_shapes_identical_with_flow(grid):
+    """2-D wave tiles (R = 2, 4, 8) write the same frames, potential and flow planes as the
+    256-cell chunks, in full and newest-only launches (G = 96: only R = 8 tiles apply; G = 100:
+    none does, the chunks run)."""
+    from flow_field_based_motion_planner_amd import _abi
+    cfg = FFMPConfig(grid=grid, n_obst=32, n_beams=0, moving=True, obst_rmax=0.6, obst_vmax=1.5, flow=True,
+                     world_half=grid * 0.05 * 0.75, max_steps=4, seed=grid)
+    shapes = [(2048, 0), (2048, _abi.RASTER_TILE2), (2048, _abi.RASTER_TILE4), (4096, _abi.RASTER_TILE8),
+              (16384, _abi.RASTER_TILE4 | _abi.RASTER_NT), (8192, _abi.RASTER_TILE4 | _abi.RASTER_XCD)]
+    ref = None
+    for shape in shapes:
+        env = FFMPVec(11, cfg, device="cuda:0", autotune=False, frame_window=4)
+        env.raster_shape = env.raster_shape_newest = shape
+        env.reset()
+        gen = torch.Generator(device="cuda:0").manual_seed(3)
+        outs = []
+        for _ in range(7):
+            o, _, _, _ = env.step(torch.randint(0, 28, (11,), device="cuda:0", generator=gen))
+            outs.append((o["state_m"].clone(), o["potential"].clone(), o["flow"].clone()))
+        if ref is None:
+            ref = outs
+        for got, want in zip(outs, ref):
+            for a, b in zip(got, want):
+                assert torch.equal(a, b), shape
 
 
 def test_newest_only_shapes_identical():

@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=16,
                    help="processes of the parallel CPU baseline (SURVEY 8d (ii); capped at the host's CPUs, 0 = skip)")
     p.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--dump-launches", action="store_true", help="print every timed raster launch (ms) to stderr")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
     p.add_argument("--frame-window", type=int, default=None,
@@ -212,6 +213,8 @@ def main():
     # launch from the frame-window schedule (full launches write both frames), plus the older
     # frame of every env reset during a newest-only launch (resets spread evenly over launches)
     r_ms = [r[0].elapsed_time(r[1]) for r in raster_ev]
+    if args.dump_launches:
+        print("raster ms per launch:", " ".join(f"{x:.3f}" for x in r_ms), file=sys.stderr, flush=True)
     n_full = sum(1 for r in raster_ev if r[4])
     G2 = cfg.grid * cfg.grid
     r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * 4 * G2

@@ -110,7 +110,9 @@ _SIGS = {
     "ffmp_episode_init": (C.c_int, [_I64, _P, _I32, C.POINTER(EpisodeT), _P]),
     "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
                                       _P]),
-    "ffmp_ring_create": (C.c_int, [_I32, _I64, _I32, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
+    "ffmp_ring_create": (C.c_int, [_I32, _I64, _I32, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
+    "ffmp_ring_info": (C.c_int, [_P, C.POINTER(C.c_double), _I32]),
+    "ffmp_ring_rebuild": (C.c_int, [_P, C.c_uint64, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "ffmp_ring_destroy": (C.c_int, [_P]),
     "ffmp_ring_pool_bytes": (_I64, [_I32]),
     "ffmp_dlpack": (_P, [_P, _I32, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64), _I32, _P]),
@@ -225,32 +227,77 @@ def tensor_from_pointer(ptr: int, shape, strides, device_type: int = DL_ROCM, de
 
 
 class SeamlessRing:
-    """`slots` frame planes of `slot_bytes` in device memory plus a virtual slot `slots` that is a
-    second mapping of slot 0 (include/ffmp.h ffmp_ring_create), handed to torch as ONE tensor
-    (slots + 1, *plane) with the slot stride.  The mapping is released when that tensor and
-    every view of it are freed."""
+    """`slots` frame planes of `plane_shape` in device memory plus a virtual slot `slots` that is
+    a second mapping of slot 0 (include/ffmp.h ffmp_ring_create), handed to torch as ONE tensor
+    (slots + 1, *plane) with the slot stride.  `partner`: the tensor the raster writes in
+    lockstep with each slot (the potential plane; its contents are overwritten) — slot pieces
+    are chosen to pair well with it.  The ring's pieces return to the process pool when its
+    tensor and every view of it are freed (and the SeamlessRing object is gone)."""
 
-    @staticmethod
-    def tensor(device_id: int, plane_shape, slots: int, bits: int = 32):
-        lib = load()
-        esize = bits // 8
-        slot_bytes = esize
+    def __init__(self, device_id: int, plane_shape, slots: int, bits: int = 32, partner=None):
+        self.lib = load()
+        self.device_id, self.plane_shape, self.slots, self.bits = int(device_id), tuple(plane_shape), int(slots), bits
+        slot_bytes = bits // 8
         for d in plane_shape:
             slot_bytes *= int(d)
         ring, base, stride = _P(), _P(), _I64()
-        check(lib.ffmp_ring_create(int(device_id), int(slot_bytes), int(slots), C.byref(ring), C.byref(base),
-                                   C.byref(stride)), "ffmp_ring_create")
+        pp, pb = self._partner(partner)
+        check(self.lib.ffmp_ring_create(self.device_id, int(slot_bytes), self.slots, pp, pb, C.byref(ring),
+                                        C.byref(base), C.byref(stride)), "ffmp_ring_create")
+        self.handle = None
+        self.tensor = None
+        self.rebuilds = 0
+        self._adopt(ring, base, stride)
+
+    @staticmethod
+    def _partner(partner):
+        if partner is None:
+            return None, 0
+        return partner.data_ptr(), partner.numel() * partner.element_size()
+
+    def _adopt(self, ring, base, stride) -> None:
+        """Wrap a fresh ring as the (slots + 1, *plane) tensor; this object keeps the creator's
+        reference (the handle) so the ring can be rebuilt."""
+        esize = self.bits // 8
         try:
             inner = [1]
-            for d in reversed(plane_shape[1:]):
+            for d in reversed(self.plane_shape[1:]):
                 inner.insert(0, inner[0] * int(d))
-            shape = (int(slots) + 1,) + tuple(int(d) for d in plane_shape)
+            shape = (self.slots + 1,) + self.plane_shape
             strides = (stride.value // esize,) + tuple(inner)
-            t = tensor_from_pointer(base.value, shape, strides, DL_ROCM, int(device_id), bits, owner=ring.value)
-            t[:slots].zero_()  # stream-ordered with the launches that follow
-        finally:
-            lib.ffmp_ring_destroy(ring)  # the creator's reference; the tensor holds its own
-        return t, stride.value
+            t = tensor_from_pointer(base.value, shape, strides, DL_ROCM, self.device_id, self.bits, owner=ring.value)
+            t[:self.slots].zero_()  # stream-ordered with the launches that follow
+        except Exception:
+            self.lib.ffmp_ring_destroy(ring)
+            raise
+        old = self.handle
+        self.handle, self.tensor, self.slot_stride = ring.value, t, stride.value
+        if old is not None:
+            self.lib.ffmp_ring_destroy(C.c_void_p(old))
+
+    def rebuild(self, slot_mask: int, partner=None) -> None:
+        """Replace the pieces of the slots in slot_mask (ffmp_ring_rebuild); `tensor` becomes a new
+        tensor — views of the old one must not be used any more."""
+        ring, base, stride = _P(), _P(), _I64()
+        pp, pb = self._partner(partner)
+        check(self.lib.ffmp_ring_rebuild(C.c_void_p(self.handle), int(slot_mask), pp, pb, C.byref(ring),
+                                         C.byref(base), C.byref(stride)), "ffmp_ring_rebuild")
+        self.rebuilds += 1
+        self._adopt(ring, base, stride)
+
+    def info(self) -> dict:
+        out = (C.c_double * 5)()
+        self.lib.ffmp_ring_info(C.c_void_p(self.handle), out, 5)
+        return {"pieces": int(out[0]), "pieces_new": int(out[1]), "pair_probes": int(out[2]),
+                "pair_gbs_min": round(out[3], 1), "pair_gbs_max": round(out[4], 1), "rebuilds": self.rebuilds}
+
+    def __del__(self):
+        try:
+            if self.handle is not None:
+                self.lib.ffmp_ring_destroy(C.c_void_p(self.handle))
+                self.handle = None
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 def footprint_from_lib(grid: int, res: float, robot_r: float):

@@ -19,6 +19,8 @@
 #include <stddef.h>
 #include <string.h>
 
+#include <algorithm>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -1034,26 +1036,43 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
 }  // extern "C"
 
 // ------------------------------------------------------------------ seamless frame ring
-// Physical: slot 0 (its own handle, so it can be mapped twice with offset 0 — hipMemMap's
-// offset must be 0) and slots 1..W-1 (one handle).  Virtual: [slot 0 | slots 1..W-1 | slot 0].
+// Built from physical PIECES (hipMemCreate handles of piece_bytes): slot i of the ring is n
+// pieces mapped back to back, and virtual slot W maps slot 0's pieces a second time (the
+// alias).  Two findings on MI355X / ROCm 7.2 shape it:
 //
-// Rings are never unmapped while the process runs.  On ROCm 7.x, once a VMM range has been
-// unmapped and its address freed, a later mapping at a reused address is not reliably what the
-// runtime resolves: a kernel whose pointer argument falls in the reused range, or a copy from
-// it, can reach the OLD allocation (tools/ring_reuse_probe.hip: D2H copies of a fresh mapping
-// return the previous ring's bytes, with or without the alias; FFMPVec saw the first raster
-// into a fresh ring vanish).  So a destroyed ring — the last reference dropped — is parked in
-// a process-wide pool and handed out again to the next ring of the same device and slot count
-// whose slots fit its stride; nothing is ever returned to the driver before exit.
+// * Pairing.  The raster writes a frame slot and the potential plane in lockstep (same offset,
+//   same time).  Two lockstep store streams run at ~6.9 TB/s or at 4.6-5.6 TB/s depending on
+//   the PHYSICAL memory each lands in (tools/pair_alias_probe.hip: two virtual mappings of the
+//   same pages pair identically; tools/region_probe.hip), so one slot that pairs badly with
+//   the potential plane makes one step in W ~25 % slower.  With a `partner` (the potential
+//   plane), every piece position (slot i, piece j) gets a piece measured to pair well with the
+//   partner's bytes [j*P, (j+1)*P): a two-stream store probe, candidates from the free-piece
+//   pool first, then fresh pieces; pieces that pair badly here stay pooled for other positions
+//   or later rings.
+// * Never unmap.  Once a VMM range is unmapped and its address reused by a new mapping, the
+//   runtime can still resolve the address to the OLD allocation (tools/ring_reuse_probe.hip:
+//   D2H copies of a fresh mapping return the previous ring's bytes; FFMPVec saw the first
+//   raster into a fresh ring vanish).  So nothing is ever unmapped before exit: every piece
+//   keeps a private "home" mapping, a ring maps its pieces once more at a fresh address, and a
+//   ring whose last reference is dropped returns its pieces to the pool (its addresses are
+//   simply never used again).
+struct ffmp_piece {
+  hipMemGenericAllocationHandle_t h;
+  char* home;  // private mapping, for the pairing probe
+  size_t bytes;
+  int32_t device;
+};
+
 struct ffmp_ring {
   int32_t device;
   int32_t slots;
-  size_t stride;
+  size_t stride;  // slot stride = pieces_per_slot * piece bytes
   char* va;
   size_t vbytes;
-  hipMemGenericAllocationHandle_t h0, h1;
-  int mapped;  // bit 0: slot 0, bit 1: slots 1..W-1, bit 2: the alias
-  int refs;    // the creator + one per live DLPack tensor (atomic); 0 = parked in the pool
+  int refs;  // the creator + one per live DLPack tensor (atomic)
+  std::vector<ffmp_piece> pieces;  // slot-major, slots * pieces_per_slot
+  double pair_gbs_min, pair_gbs_max;  // pairing probe of the chosen pieces (0 without partner)
+  int pieces_new, pieces_tested;
 };
 
 // dlpack.h (v0.8) DLManagedTensor, the interchange torch.utils.dlpack.from_dlpack consumes
@@ -1079,27 +1098,82 @@ struct DLHolder_ {  // one allocation: the managed tensor, its shape/strides, it
   ffmp_ring* owner;
 };
 
+// two lockstep 16-B nontemporal store streams over n16 float4s: the raster's write pattern
+__global__ __launch_bounds__(256) void pair_probe_kernel(f32x4* __restrict__ a, f32x4* __restrict__ b, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 4096 + threadIdx.x; i < n16 && i < ((int64_t)blockIdx.x + 1) * 4096; i += 256) {
+    const f32x4 x = {0.f, 1.f, 2.f, 3.f};
+    __builtin_nontemporal_store(x, a + i);
+    __builtin_nontemporal_store(x, b + i);
+  }
+}
+
 namespace {
 
 std::mutex g_pool_mu;
-std::vector<ffmp_ring*> g_pool;  // parked rings (refs == 0), mapped, reusable
+std::vector<ffmp_piece> g_pieces;  // free pieces (mapped at home), reusable
 
-// Only for a ring whose creation failed half-way (never used by a launch): unmap what was
-// mapped and give it back.
-void ring_undo(ffmp_ring* r) {
-  if (r->mapped & 4) (void)hipMemUnmap(r->va + r->stride * r->slots, r->stride);
-  if (r->mapped & 2) (void)hipMemUnmap(r->va + r->stride, r->stride * (r->slots - 1));
-  if (r->mapped & 1) (void)hipMemUnmap(r->va, r->stride);
-  if (r->va) (void)hipMemAddressFree(r->va, r->vbytes);
-  if (r->h1) (void)hipMemRelease(r->h1);
-  if (r->h0) (void)hipMemRelease(r->h0);
-  delete r;
+hipMemAllocationProp dev_prop(int32_t device) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  return prop;
+}
+
+hipError_t map_rw(char* va, size_t bytes, hipMemGenericAllocationHandle_t h, int32_t device) {
+  hipError_t e = hipMemMap(va, bytes, 0, h, 0);
+  if (e != hipSuccess) return e;
+  hipMemAccessDesc acc = {};
+  acc.location = dev_prop(device).location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  return hipMemSetAccess(va, bytes, &acc, 1);
+}
+
+// a fresh piece mapped at its home address; on failure nothing stays allocated
+hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out) {
+  hipMemAllocationProp prop = dev_prop(device);
+  ffmp_piece p = {};
+  p.bytes = bytes;
+  p.device = device;
+  hipError_t e = hipMemCreate(&p.h, bytes, &prop, 0);
+  if (e != hipSuccess) return e;
+  if ((e = hipMemAddressReserve((void**)&p.home, bytes, std::max(gran, std::min(bytes, (size_t)1 << 30)), nullptr, 0)) !=
+      hipSuccess) {
+    (void)hipMemRelease(p.h);  // never mapped: safe to give back
+    return e;
+  }
+  if ((e = map_rw(p.home, bytes, p.h, device)) != hipSuccess) {
+    (void)hipMemUnmap(p.home, bytes);
+    (void)hipMemAddressFree(p.home, bytes);
+    (void)hipMemRelease(p.h);
+    return e;
+  }
+  *out = p;
+  return hipSuccess;
+}
+
+// GB/s of the two-stream store probe over `bytes` of piece home + partner range
+double pair_gbs(char* a, char* b, size_t bytes, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  const int64_t n16 = (int64_t)(bytes / 16);
+  const unsigned blocks = (unsigned)((n16 + 4095) / 4096);
+  float best = 1e30f;
+  for (int r = 0; r < 4; ++r) {
+    (void)hipEventRecord(e0, s);
+    hipLaunchKernelGGL(pair_probe_kernel, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
+    (void)hipEventRecord(e1, s);
+    if (hipEventSynchronize(e1) != hipSuccess) return 0.0;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (r > 0 && ms < best) best = ms;  // first launch warms up
+  }
+  return 2.0 * (double)(n16 * 16) / (best * 1e-3) / 1e9;
 }
 
 void ring_unref(ffmp_ring* r) {
   if (__atomic_sub_fetch(&r->refs, 1, __ATOMIC_ACQ_REL) > 0) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(r);
+  for (const ffmp_piece& p : r->pieces) g_pieces.push_back(p);  // the ring's addresses are retired
+  delete r;
 }
 
 // restores the caller's current device on scope exit
@@ -1118,82 +1192,241 @@ struct DeviceScope {
 
 extern "C" {
 
-int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, ffmp_ring_t** ring, void** base,
-                     int64_t* slot_stride) {
+}  // extern "C"
+
+namespace {
+
+struct RingGeom {
+  size_t gran, piece, stride;
+  int per_slot;
+  bool pairing;
+};
+
+int ring_geom(int32_t device, int64_t slot_bytes, const void* partner, RingGeom* g) {
+  int vmm = 0;
+  if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
+    return fail(FFMP_E_HIP, "ffmp_ring: device %d has no virtual memory management", device);
+  hipMemAllocationProp prop = dev_prop(device);
+  hipError_t e = hipMemGetAllocationGranularity(&g->gran, &prop, hipMemAllocationGranularityMinimum);
+  if (e != hipSuccess || g->gran == 0) return fail(FFMP_E_HIP, "hipMemGetAllocationGranularity: %s", hipGetErrorString(e));
+  // pieces: 1 GiB for slots of >= 2 GiB (the pairing resolution), else one piece per slot
+  const size_t slot_g = ((size_t)slot_bytes + g->gran - 1) / g->gran * g->gran;
+  g->piece = slot_g >= (2ull << 30) ? (1ull << 30) : slot_g;
+  g->per_slot = (int)((slot_g + g->piece - 1) / g->piece);
+  g->stride = g->piece * (size_t)g->per_slot;
+  g->pairing = partner != nullptr && g->piece >= (256ull << 20);
+  return FFMP_OK;
+}
+
+void pool_put(const std::vector<ffmp_piece>& v) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (const ffmp_piece& p : v) g_pieces.push_back(p);
+}
+
+// Pieces beyond the ones a ring needs (pairing candidates) only while the device keeps
+// max(8 GiB, 5 %) free beside them.
+bool room_for(size_t bytes) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
+  const size_t reserve = std::max((size_t)8 << 30, total_b / 20);
+  return free_b > bytes + reserve;
+}
+
+// Fill r->pieces[pos] for every pos with need[pos] set: candidates from the pool first (at most
+// 6 per position), then fresh pieces; with a partner, the first piece whose two-stream store
+// probe against the partner bytes at the same offset is within 7 % of the best probe seen
+// (after >= 3 probes), else the best of 12.  `avoid` pieces are not candidates (they go to the
+// pool afterwards).
+int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
+                  int64_t partner_bytes, const std::vector<ffmp_piece>& avoid) {
+  const int32_t device = r->device;
+  std::vector<ffmp_piece> cand;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t k = 0; k < g_pieces.size();) {
+      if (g_pieces[k].device == device && g_pieces[k].bytes == g.piece) {
+        cand.push_back(g_pieces[k]);
+        g_pieces.erase(g_pieces.begin() + k);
+      } else {
+        ++k;
+      }
+    }
+  }
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  struct Cleanup {
+    hipStream_t& s; hipEvent_t& a; hipEvent_t& b;
+    ~Cleanup() { if (a) (void)hipEventDestroy(a); if (b) (void)hipEventDestroy(b); if (s) (void)hipStreamDestroy(s); }
+  } cleanup{s, e0, e1};
+  if (g.pairing && (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) {
+    pool_put(cand);
+    return fail(FFMP_E_HIP, "ffmp_ring: stream/event creation failed");
+  }
+  int todo = 0;
+  for (char n : need) todo += n != 0;
+  const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
+  double ref = 0.0;                          // best probe seen: the scale "fast" is judged against
+  int fresh = 0;
+  hipError_t e = hipSuccess;
+  for (size_t pos = 0; pos < need.size(); ++pos) {
+    if (!need[pos]) continue;
+    const int j = (int)(pos % (size_t)g.per_slot);
+    const size_t off = (size_t)j * g.piece;
+    char* pb = g.pairing ? (char*)partner + off : nullptr;
+    const size_t pbytes = g.pairing && (int64_t)off < partner_bytes ? std::min(g.piece, (size_t)(partner_bytes - (int64_t)off)) : 0;
+    const bool test = g.pairing && pbytes >= (64u << 20);
+    int pick = -1, here = 0;
+    double pick_gbs = -1.0;
+    size_t k = 0;
+    for (;;) {
+      int c = -1;
+      if (k < cand.size() && k < 6) {
+        c = (int)k++;
+      } else if (fresh < max_new && (fresh < todo || room_for(g.piece))) {
+        ffmp_piece p;
+        if ((e = new_piece(device, g.piece, g.gran, &p)) != hipSuccess) {
+          (void)hipGetLastError();
+          if (pick >= 0 || !cand.empty()) break;  // out of memory: settle for what there is
+          pool_put(cand);
+          return fail(FFMP_E_HIP, "ffmp_ring: hipMemCreate/map of a %zu-byte piece: %s", g.piece, hipGetErrorString(e));
+        }
+        ++fresh;
+        cand.push_back(p);
+        c = (int)cand.size() - 1;
+        k = cand.size();
+      } else {
+        break;
+      }
+      if (!test) {
+        pick = c;
+        break;
+      }
+      const double gbs = pair_gbs(cand[c].home, pb, pbytes, s, e0, e1);
+      ++r->pieces_tested;
+      ++here;
+      if (gbs > ref) ref = gbs;
+      if (gbs > pick_gbs) {
+        pick = c;
+        pick_gbs = gbs;
+      }
+      if (r->pieces_tested >= 3 && pick_gbs >= 0.93 * ref) break;
+      if (here >= 12) break;  // bounded search: keep the best seen
+    }
+    if (pick < 0) {
+      pool_put(cand);
+      return fail(FFMP_E_HIP, "ffmp_ring: no piece available");
+    }
+    if (test) {
+      r->pair_gbs_min = r->pair_gbs_min > 0 ? std::min(r->pair_gbs_min, pick_gbs) : pick_gbs;
+      r->pair_gbs_max = std::max(r->pair_gbs_max, pick_gbs);
+    }
+    r->pieces[pos] = cand[pick];
+    cand.erase(cand.begin() + pick);
+  }
+  r->pieces_new += fresh;
+  pool_put(cand);
+  pool_put(avoid);
+  return FFMP_OK;
+}
+
+// reserve the ring's own addresses and map slots 0..W-1, then slot 0's pieces again
+int ring_map(ffmp_ring* r, const RingGeom& g) {
+  // aligned to the piece (up to 1 GiB) so that every piece maps with the largest page fragments
+  hipError_t e = hipMemAddressReserve((void**)&r->va, r->vbytes, std::max(g.gran, std::min(g.piece, (size_t)1 << 30)),
+                                      nullptr, 0);
+  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipMemAddressReserve: %s", hipGetErrorString(e));
+  for (int v = 0; v <= r->slots; ++v) {
+    const int slot = v % r->slots;
+    for (int j = 0; j < g.per_slot; ++j) {
+      const ffmp_piece& p = r->pieces[(size_t)slot * g.per_slot + j];
+      if ((e = map_rw(r->va + (size_t)v * r->stride + (size_t)j * g.piece, g.piece, p.h, r->device)) != hipSuccess)
+        return fail(FFMP_E_HIP, "ffmp_ring: hipMemMap: %s", hipGetErrorString(e));  // never reused
+    }
+  }
+  return FFMP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const void* partner, int64_t partner_bytes,
+                     ffmp_ring_t** ring, void** base, int64_t* slot_stride) {
   if (!ring || !base || !slot_stride) return fail(FFMP_E_ARG, "ffmp_ring_create: NULL output pointer");
   *ring = nullptr;
   *base = nullptr;
   if (slot_bytes <= 0 || slots < 2) return fail(FFMP_E_ARG, "ffmp_ring_create: slot_bytes > 0 and slots >= 2 required");
-  {  // a parked ring of this shape: the tightest fit
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    size_t best = (size_t)-1, at = 0;
-    for (size_t k = 0; k < g_pool.size(); ++k) {
-      const ffmp_ring* p = g_pool[k];
-      if (p->device == device && p->slots == slots && p->stride >= (size_t)slot_bytes && p->stride < best &&
-          p->stride <= 2 * (size_t)slot_bytes + (2u << 20)) {
-        best = p->stride;
-        at = k;
-      }
-    }
-    if (best != (size_t)-1) {
-      ffmp_ring* r = g_pool[at];
-      g_pool.erase(g_pool.begin() + at);
-      r->refs = 1;
-      *ring = r;
-      *base = r->va;
-      *slot_stride = (int64_t)r->stride;
-      return FFMP_OK;
-    }
-  }
+  if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_create: partner_bytes must be > 0");
   DeviceScope scope(device);
-  int vmm = 0;
-  if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
-    return fail(FFMP_E_HIP, "ffmp_ring_create: device %d has no virtual memory management", device);
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = device;
-  size_t gran = 0;
-  hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
-  if (e != hipSuccess || gran == 0) return fail(FFMP_E_HIP, "hipMemGetAllocationGranularity: %s", hipGetErrorString(e));
-  ffmp_ring* r = new ffmp_ring();
+  RingGeom g;
+  if (const int rc = ring_geom(device, slot_bytes, partner, &g)) return rc;
+  std::unique_ptr<ffmp_ring> r(new ffmp_ring());
   r->device = device;
   r->slots = slots;
-  r->stride = ((size_t)slot_bytes + gran - 1) / gran * gran;
-  r->vbytes = r->stride * (size_t)(slots + 1);
-  const char* what = "hipMemCreate";
-  if ((e = hipMemCreate(&r->h0, r->stride, &prop, 0)) != hipSuccess) goto fail_;
-  if ((e = hipMemCreate(&r->h1, r->stride * (size_t)(slots - 1), &prop, 0)) != hipSuccess) goto fail_;
-  what = "hipMemAddressReserve";
-  if ((e = hipMemAddressReserve((void**)&r->va, r->vbytes, gran, nullptr, 0)) != hipSuccess) {
-    r->va = nullptr;
-    goto fail_;
-  }
-  what = "hipMemMap";
-  if ((e = hipMemMap(r->va, r->stride, 0, r->h0, 0)) != hipSuccess) goto fail_;
-  r->mapped |= 1;
-  if ((e = hipMemMap(r->va + r->stride, r->stride * (size_t)(slots - 1), 0, r->h1, 0)) != hipSuccess) goto fail_;
-  r->mapped |= 2;
-  what = "hipMemMap (alias of slot 0)";
-  if ((e = hipMemMap(r->va + r->stride * (size_t)slots, r->stride, 0, r->h0, 0)) != hipSuccess) goto fail_;
-  r->mapped |= 4;
-  {
-    hipMemAccessDesc acc = {};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    what = "hipMemSetAccess";
-    if ((e = hipMemSetAccess(r->va, r->vbytes, &acc, 1)) != hipSuccess) goto fail_;
+  r->stride = g.stride;
+  r->vbytes = g.stride * (size_t)(slots + 1);
+  r->pieces.resize((size_t)slots * g.per_slot);
+  const std::vector<char> need(r->pieces.size(), 1);
+  if (const int rc = choose_pieces(r.get(), g, need, (const char*)partner, partner_bytes, {})) return rc;
+  if (const int rc = ring_map(r.get(), g)) {
+    pool_put(r->pieces);
+    return rc;
   }
   r->refs = 1;
-  *ring = r;
   *base = r->va;
   *slot_stride = (int64_t)r->stride;
+  *ring = r.release();
   return FFMP_OK;
-fail_:
-  fail(FFMP_E_HIP, "ffmp_ring_create: %s: %s", what, hipGetErrorString(e));
-  (void)hipGetLastError();
-  ring_undo(r);
-  return FFMP_E_HIP;
+}
+
+int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partner, int64_t partner_bytes,
+                      ffmp_ring_t** ring, void** base, int64_t* slot_stride) {
+  if (!old || !ring || !base || !slot_stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: NULL argument");
+  *ring = nullptr;
+  *base = nullptr;
+  if (old->slots > 64) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: more than 64 slots");
+  if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: partner_bytes must be > 0");
+  DeviceScope scope(old->device);
+  RingGeom g;
+  if (const int rc = ring_geom(old->device, (int64_t)old->stride, partner, &g)) return rc;
+  if (g.stride != old->stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: geometry changed");
+  std::unique_ptr<ffmp_ring> r(new ffmp_ring());
+  r->device = old->device;
+  r->slots = old->slots;
+  r->stride = old->stride;
+  r->vbytes = old->vbytes;
+  r->pieces.resize(old->pieces.size());
+  std::vector<char> need(r->pieces.size(), 0);
+  std::vector<ffmp_piece> avoid, keep;
+  for (size_t pos = 0; pos < old->pieces.size(); ++pos) {
+    const int slot = (int)(pos / (size_t)g.per_slot);
+    if ((replace_mask >> slot) & 1u) {
+      need[pos] = 1;
+      avoid.push_back(old->pieces[pos]);
+    } else {
+      r->pieces[pos] = old->pieces[pos];
+    }
+  }
+  if (const int rc = choose_pieces(r.get(), g, need, (const char*)partner, partner_bytes, avoid)) return rc;
+  if (const int rc = ring_map(r.get(), g)) {
+    // the kept pieces still belong to `old`; give back only the new ones
+    std::vector<ffmp_piece> fresh;
+    for (size_t pos = 0; pos < need.size(); ++pos)
+      if (need[pos]) fresh.push_back(r->pieces[pos]);
+    pool_put(fresh);
+    return rc;
+  }
+  // ownership: `old` keeps nothing (its replaced pieces are pooled, its kept ones moved here);
+  // its addresses stay mapped and are never used again
+  old->pieces.clear();
+  r->pieces_new += old->pieces_new;
+  r->pieces_tested += old->pieces_tested;
+  r->refs = 1;
+  *base = r->va;
+  *slot_stride = (int64_t)r->stride;
+  *ring = r.release();
+  return FFMP_OK;
 }
 
 int ffmp_ring_destroy(ffmp_ring_t* ring) {
@@ -1201,11 +1434,21 @@ int ffmp_ring_destroy(ffmp_ring_t* ring) {
   return FFMP_OK;
 }
 
+int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap) {
+  if (!ring || !out || cap < 5) return fail(FFMP_E_ARG, "ffmp_ring_info: ring/out NULL or cap < 5");
+  out[0] = (double)ring->pieces.size();
+  out[1] = (double)ring->pieces_new;
+  out[2] = (double)ring->pieces_tested;
+  out[3] = ring->pair_gbs_min;
+  out[4] = ring->pair_gbs_max;
+  return 5;
+}
+
 int64_t ffmp_ring_pool_bytes(int32_t device) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   int64_t b = 0;
-  for (const ffmp_ring* p : g_pool)
-    if (p->device == device || device < 0) b += (int64_t)(p->stride * (size_t)p->slots);
+  for (const ffmp_piece& p : g_pieces)
+    if (p.device == device || device < 0) b += (int64_t)p.bytes;
   return b;
 }
 

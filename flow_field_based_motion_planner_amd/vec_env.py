@@ -99,6 +99,7 @@ class FFMPVec:
         if seamless and self.frame_window == 2:
             raise ValueError("seamless=True needs frame_window > 2")
         self.ring = "contiguous" if self.frame_window == 2 else "wrap"  # or "seamless" (set by _alloc)
+        self.ring_meta = None
         self._wpos = 0  # frame slot of state_m[:, 0]
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
@@ -112,8 +113,15 @@ class FFMPVec:
                                    torch.float32)
         if autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
             self._autotune_raster()
-            if self.arena and plane_bytes >= self.REPLACE_MIN_BYTES:
+            # the seamless ring already paired its slots with the potential plane; a new arena
+            # would undo that
+            paired = self.ring == "seamless" and self.with_potential
+            if self.arena and plane_bytes >= self.REPLACE_MIN_BYTES and not paired:
                 self._retry_placement()
+            if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
+                self._repair_slots()
+            if self.placement is not None and self.ring_meta is not None:
+                self.placement = dict(self.placement, ring=self.ring_meta)
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
@@ -172,33 +180,34 @@ class FFMPVec:
 
     def _alloc_ring(self) -> bool:
         """The seamless frame ring (HIP VMM, virtual slot W aliasing slot 0), if requested and
-        the device supports it."""
-        self._ring_stride = None
-        if self._seamless_req is False:
-            return False
+        the device supports it; its slots are built to pair well with the potential plane the
+        raster writes beside them (include/ffmp.h ffmp_ring_create)."""
         N, G = self.num_envs, self.cfg.grid
         try:
-            self.frames, stride = _abi.SeamlessRing.tensor(self.device.index, (N, G, G), self.frame_window)
+            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, partner=self.potential)
+            self.frames = self._ring.tensor
+            self.ring_meta = self._ring.info()
         except _abi.FFMPBackendError:
             if self._seamless_req:
                 raise
             self._seamless_req = False  # no VMM here: the wrapping ring from now on
             return False
-        self._ring_stride = stride
         self.ring = "seamless"
         return True
 
     def _alloc(self, keep_ring: bool = False):
         """All per-shard buffers, zero-initialised.  With arena=True (default) they are views
-        into ONE device allocation carved at 2 MiB boundaries, planes first (the seamless frame
-        ring, when used, is its own VMM mapping; keep_ring: re-allocate everything else)."""
+        into ONE device allocation carved at 2 MiB boundaries, planes first.  The seamless frame
+        ring, when used, is its own VMM allocation, made after the arena so that its slots can
+        be paired with the potential plane (keep_ring: re-allocate everything else)."""
         dev = self.device
-        if keep_ring and self.ring == "seamless":
-            seamless = True
-        else:
+        keep = keep_ring and self.ring == "seamless"
+        want_ring = keep or self._seamless_req is not False
+        if not keep:
             self.frames = None
-            seamless = self._alloc_ring()
-        specs = self._buffer_specs(with_frames=not seamless)
+            self._ring = None
+            self.ring_meta = None
+        specs = self._buffer_specs(with_frames=not want_ring)
         self.potential = None
         self.lidar = None
         self.flow = None
@@ -212,12 +221,16 @@ class FFMPVec:
                 off += self._nbytes(shape, dtype)
             self._arena_used = -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN
             self._arena_buf = torch.zeros(max(self._arena_used, 1), dtype=torch.uint8, device=dev)
-            self._carve(0)
+            self._carve(0, specs)
         else:
             self._arena_buf = None
             self._arena_used = 0
             for name, shape, dtype in specs:
                 setattr(self, name, torch.zeros(shape, dtype=dtype, device=dev))
+        if want_ring and not keep and not self._alloc_ring():
+            return self._alloc()  # no VMM: the wrapping ring, frames in the arena
+        if self.potential is not None:
+            self.potential.zero_()  # the pairing probe wrote into it
         L = self.cfg.n_beams
         self.beam_cs = torch.as_tensor(beam_table(L), dtype=torch.float64).to(dev) if L > 0 else None
 
@@ -228,10 +241,10 @@ class FFMPVec:
             n *= d
         return n * torch.empty((), dtype=dtype).element_size()
 
-    def _carve(self, base: int) -> None:
-        """Point every buffer into the arena, starting `base` bytes in."""
+    def _carve(self, base: int, specs) -> None:
+        """Point every buffer of `specs` into the arena, starting `base` bytes in."""
         self._arena_base = base
-        for (name, shape, dtype), o in zip(self._buffer_specs(with_frames=self.ring != "seamless"), self._arena_offs):
+        for (name, shape, dtype), o in zip(specs, self._arena_offs):
             nb = self._nbytes(shape, dtype)
             setattr(self, name, self._arena_buf[base + o:base + o + nb].view(dtype).view(shape))
 
@@ -278,53 +291,123 @@ class FFMPVec:
                 out[full] = (sum(r[3] for r in sel) / (ms * 1e-3) / 1e9, ms / len(sel))
         return out
 
-    # Placement retries.  Even the best shape runs ~15 % slower on a "slow" placement (e.g.
-    # C3: 6.2-6.3 vs 7.1-7.3 TB/s), and allocating again while the first arena and a spacer
-    # are still held (so the allocator must return different memory) often lands fast.  If the
-    # tuned bandwidth is below PLACEMENT_FAST_GBS, up to PLACEMENT_RETRIES further arenas are
-    # tried (each autotuned) and the fastest kept; bounded by free HBM.
+    # Placement retries.  Two planes written in lockstep (a frame slot and the potential plane)
+    # stream at ~7.1 TB/s or ~5.3-6.2 depending on where each landed in physical memory — a
+    # property of the PAIR (tools/region_probe.hip, profiles/r01_ring.txt §6) — so with the
+    # seamless ring one slow slot/plane pair makes one step in W ~25 % slower.  Allocating again
+    # while the earlier arenas and a spacer are still held (so the allocator must return
+    # different memory) often lands fast: below the threshold, up to PLACEMENT_RETRIES further
+    # arenas are timed over one whole ring cycle and the fastest kept; bounded by free HBM.
     REPLACE_MIN_BYTES = 4 << 30
     PLACEMENT_FAST_GBS = 6800.0
-    PLACEMENT_RETRIES = 3
+    PLACEMENT_FAST_GBS_SEAMLESS = 7000.0  # newest-only launches only: every slot paired well
+    PLACEMENT_RETRIES = 8
     PLACEMENT_SPACER = 1 << 30
 
     def _retry_placement(self) -> None:
+        """Below the fast threshold, allocate the arena again (the seamless ring is kept: rings are
+        never unmapped) while the previous ones and a growing spacer are held, time one ring
+        cycle with the tuned shapes, keep the fastest; then re-tune the shapes on the winner."""
         names = [n for n, _, _ in self._buffer_specs()]  # includes "frames" (arena or ring)
-        keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
-                 (self.raster_shape, self.raster_shape_newest), self.placement, self._ring_stride)]
+        keep = [(self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names})]
         spacers = []
         tries = [round(self.placement["gbs"], 1)]
+        fast = self.PLACEMENT_FAST_GBS_SEAMLESS if self.ring == "seamless" else self.PLACEMENT_FAST_GBS
         for k in range(self.PLACEMENT_RETRIES):
-            if max(c[0] for c in keep) >= self.PLACEMENT_FAST_GBS:
+            if max(c[0] for c in keep) >= fast:
                 break
             free, _ = torch.cuda.mem_get_info(self.device)
             if free < 1.2 * self._arena_buf.numel() + (k + 1) * self.PLACEMENT_SPACER + (1 << 30):
                 break
             spacers.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
-            self._alloc(keep_ring=True)  # a seamless ring is kept (rings are never unmapped)
+            self._alloc(keep_ring=True)
             self._build_structs()
-            self._autotune_raster()
-            tries.append(round(self.placement["gbs"], 1))
-            keep.append((self.placement["gbs"], self._arena_buf, {n: getattr(self, n) for n in names},
-                         (self.raster_shape, self.raster_shape_newest), self.placement, self._ring_stride))
+            gbs = self._placement_gbs()
+            tries.append(round(gbs, 1))
+            keep.append((gbs, self._arena_buf, {n: getattr(self, n) for n in names}))
         best = max(range(len(keep)), key=lambda i: keep[i][0])
-        _, buf, views, shapes, placement, self._ring_stride = keep[best]
+        _, buf, views = keep[best]
         self._arena_buf = buf
         for n, v in views.items():
             setattr(self, n, v)
-        self.raster_shape, self.raster_shape_newest = shapes
-        self.placement = dict(placement, placement_tries=tries, placement_kept=best)
         self._build_structs()
         del keep, spacers, views, buf
         torch.cuda.empty_cache()
+        if best > 0:
+            self._autotune_raster()
+        self.placement = dict(self.placement, placement_tries=tries, placement_kept=best)
+
+    # Slot repair (seamless ring).  The pairing probe at ring creation predicts most, not all,
+    # slow slot/potential pairings; the step loop itself is the judge: time every slot's
+    # newest-only raster over two ring cycles and rebuild the ring with new pieces for slots
+    # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.
+    SLOW_SLOT = 1.06
+    REPAIR_ROUNDS = 2
+
+    def _slot_ms(self) -> Dict[int, float]:
+        """Median newest-only raster ms per physical slot written, over two ring cycles."""
+        W = self.frame_window
+        self.reset()
+        a = torch.full((self.num_envs,), 10, dtype=torch.int64, device=self.device)
+        t = []
+        for _ in range(2 * W):
+            self.step(a, timing=t)
+        torch.cuda.synchronize(self.device)
+        per: Dict[int, list] = {}
+        for k, r in enumerate(t):  # step k after a reset writes virtual slot k+1 -> physical (k+1) % W
+            per.setdefault((k + 1) % W, []).append(r[0].elapsed_time(r[1]))
+        self._clear_after_tuning()
+        return {i: float(np.median(v)) for i, v in per.items()}
+
+    def _repair_slots(self) -> None:
+        history = []
+        for _ in range(self.REPAIR_ROUNDS + 1):
+            ms = self._slot_ms()
+            fast = min(ms.values())
+            slow = [i for i, v in ms.items() if v > self.SLOW_SLOT * fast]
+            history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)], "slow": slow})
+            if not slow or len(history) > self.REPAIR_ROUNDS:
+                break
+            self._ring.rebuild(sum(1 << i for i in slow), partner=self.potential)
+            self.frames = self._ring.tensor
+            self.potential.zero_()
+            self._build_structs()
+        self.ring_meta = dict(self._ring.info(), repair=history)
+
+    def _tune_steps(self) -> int:
+        """Timed steps per measurement: >= ~10 ms of raster, in whole ring cycles — the wrapping
+        ring's W-1 steps (one full raster), or the seamless ring's W steps: every slot is written
+        once, and the potential plane streams beside each slot at its own rate (one slow
+        slot/plane pairing makes one step in W ~25 % slower, profiles/r01_ring.txt §6), so a
+        placement check must see all of them."""
+        plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) +
+                                                 (1.0 if self.flow is not None else 0.0))
+        steps = 3 if plane_bytes >= (8 << 30) else 12
+        cyc = {"wrap": self.frame_window - 1, "seamless": self.frame_window}.get(self.ring, 1)
+        return -(-steps // cyc) * cyc
+
+    def _cycle_gbs(self, ms_full: Optional[float], ms_newest: Optional[float]) -> float:
+        """Raster bandwidth of one ring cycle from per-launch times of the two kinds: one full
+        launch + W-2 newest-only ones (wrapping ring), full launches only (W = 2) or newest-only
+        ones only (seamless ring)."""
+        n_new, n_full = self.frame_window - 2, 1
+        if self.ring == "seamless":
+            n_new, n_full = 1, 0
+        b = n_full * self._raster_bytes(self.num_envs, True) + n_new * self._raster_bytes(self.num_envs, False)
+        ms = (ms_full if n_full else 0.0) + (n_new * ms_newest if n_new else 0.0)
+        return b / (ms * 1e-3) / 1e9
+
+    def _clear_after_tuning(self) -> None:
+        if self._arena_buf is not None:
+            self._arena_buf.zero_()
+        if self.ring == "seamless":
+            self.frames[:self.frame_window].zero_()
+        self._needs_reset = True
 
     def _autotune_raster(self) -> None:
         self.reset()  # a real state (a zeroed record would stack every disc on the robot cell)
         results = []
-        plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) + (1.0 if self.flow is not None else 0.0))
-        steps = 3 if plane_bytes >= (8 << 30) else 12  # >= ~10 ms of timed raster per shape
-        cyc = self.frame_window - 1 if self.ring == "wrap" else 1  # whole cycles of the wrapping ring
-        steps = -(-steps // cyc) * cyc
+        steps = self._tune_steps()
         for shape in self.RASTER_SHAPES:
             self.raster_shape = self.raster_shape_newest = shape
             results.append((self._raster_gbs_steady(steps), shape))
@@ -338,26 +421,22 @@ class FFMPVec:
         else:  # seamless ring: steps never write both frames; resets use the newest-only winner
             self.raster_shape = best[False][2]
         self.raster_shape_newest = best[False][2] if False in best else self.raster_shape
-        # the cycle's bandwidth with the chosen shapes: one full launch + W-2 newest-only ones
-        # (the wrapping ring), only full launches (W = 2) or only newest-only ones (seamless)
-        n_new = self.frame_window - 2
-        n_full = 1
-        if self.ring == "seamless":
-            n_new, n_full = 1, 0
-        b = n_full * self._raster_bytes(self.num_envs, True) + n_new * self._raster_bytes(self.num_envs, False)
-        ms = (best[True][1] if n_full else 0.0) + (n_new * best[False][1] if n_new else 0.0)
-        gbs = b / (ms * 1e-3) / 1e9
+        gbs = self._cycle_gbs(best[True][1] if True in best else None, best[False][1] if False in best else None)
         self.placement = {"shape": {"cells_per_block": self.raster_shape[0], "flags": self.raster_shape[1]},
                           "shape_newest": ({"cells_per_block": self.raster_shape_newest[0],
-                                            "flags": self.raster_shape_newest[1]} if n_new else None),
+                                            "flags": self.raster_shape_newest[1]} if False in best else None),
                           "gbs": round(gbs, 1),
                           "candidates": [[c, f] + [round(r[k][0], 1) for k in (True, False) if k in r]
                                          for r, (c, f) in results]}
-        if self._arena_buf is not None:
-            self._arena_buf.zero_()
-        if self.ring == "seamless":
-            self.frames[:self.frame_window].zero_()
-        self._needs_reset = True
+        self._clear_after_tuning()
+
+    def _placement_gbs(self) -> float:
+        """Cycle bandwidth of the current buffers with the current launch shapes."""
+        self.reset()
+        r = self._raster_gbs_steady(self._tune_steps())
+        gbs = self._cycle_gbs(r[True][1] if True in r else None, r[False][1] if False in r else None)
+        self._clear_after_tuning()
+        return gbs
 
     def _build_structs(self):
         self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)

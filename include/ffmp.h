@@ -293,20 +293,33 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
  * space over `slots` physical slots of `device` (HIP virtual memory management) and maps
  * virtual slot `slots` onto the physical pages of slot 0 a second time, so the pair [p, p+1]
  * exists for every p in [0, slots): the view slides by one slot per step forever.
- *   slot_stride = slot_bytes rounded up to the allocation granularity (out);
- *   *base = the first virtual slot (device pointer); contents undefined (zero them on the
- *   stream that will use them).
+ *   Slots are built from physical pieces (1 GiB for slots of >= 2 GiB, else one per slot);
+ *   slot_stride = slot_bytes rounded up to a whole number of pieces (out).
+ *   partner (optional, device pointer, partner_bytes): the plane the raster writes in lockstep
+ *   with every slot (the potential plane).  Two lockstep store streams run ~25 % slower when
+ *   their physical pages pair badly, so each piece position gets a piece measured (two-stream
+ *   store probe, which overwrites the partner's bytes) to pair well with the partner bytes at
+ *   the same offset.  NULL: no pairing.
+ *   *base = the first virtual slot (device pointer); contents undefined.
  * Returns 0, FFMP_E_ARG, or FFMP_E_HIP (no VMM support, out of memory, ...; then use a plain
  * ring — ffmp_last_error() says which call failed).
- * ffmp_ring_destroy drops the creator's reference.  A ring is never unmapped while the process
+ * ffmp_ring_destroy drops the creator's reference.  Nothing is ever unmapped while the process
  * runs (ROCm 7 can resolve a reused, re-mapped VMM address to the old allocation — see
- * ffmp_kernels.hip); once its last reference is gone it is parked and handed out again by the
- * next ffmp_ring_create of the same device and slot count whose slots fit its stride (up to
- * 2x + 2 MiB).  ffmp_ring_pool_bytes: physical bytes parked (device < 0: all devices). */
+ * ffmp_kernels.hip): once a ring's last reference is gone its pieces return to a process-wide
+ * pool that later rings draw from.  ffmp_ring_pool_bytes: pooled bytes (device < 0: all).
+ * ffmp_ring_info: out[0..4] = pieces, fresh pieces allocated, pairing probes, min and max
+ * probe GB/s of the chosen pieces (0 without a partner); returns 5. */
 typedef struct ffmp_ring ffmp_ring_t;
-int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, ffmp_ring_t** ring,
-                     void** base, int64_t* slot_stride);
+int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const void* partner,
+                     int64_t partner_bytes, ffmp_ring_t** ring, void** base, int64_t* slot_stride);
+/* A new ring (new addresses) with the pieces of `old`'s slots in replace_mask (bit i = slot i)
+ * replaced by other pieces (chosen as in ffmp_ring_create, never the replaced ones), the other
+ * slots' pieces moved over.  For a caller whose timing shows a slot pairing badly; `old` must
+ * not be used for data afterwards (its addresses still alias the moved pieces) — drop it. */
+int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partner, int64_t partner_bytes,
+                      ffmp_ring_t** ring, void** base, int64_t* slot_stride);
 int ffmp_ring_destroy(ffmp_ring_t* ring);
+int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap);
 int64_t ffmp_ring_pool_bytes(int32_t device);
 /* A dlpack.h (v0.8) DLManagedTensor* of float `bits` elements over `data` (element strides,
  * ndim <= 8), for consumers that take DLPack (torch.utils.dlpack.from_dlpack, CuPy, JAX).

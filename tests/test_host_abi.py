@@ -191,9 +191,13 @@ def test_ring_api_without_gpu(lib):
     """The ring helper validates its arguments and, without a GPU, fails with a message."""
     import ctypes as C
     ring, base, stride = C.c_void_p(), C.c_void_p(), C.c_int64()
-    assert lib.ffmp_ring_create(0, 0, 4, C.byref(ring), C.byref(base), C.byref(stride)) == -1
-    assert lib.ffmp_ring_create(0, 4096, 1, C.byref(ring), C.byref(base), C.byref(stride)) == -1
-    rc = lib.ffmp_ring_create(0, 1 << 20, 4, C.byref(ring), C.byref(base), C.byref(stride))
-    assert rc == -2 and not ring.value and b"ffmp_ring_create" in lib.ffmp_last_error()
+    assert lib.ffmp_ring_create(0, 0, 4, None, 0, C.byref(ring), C.byref(base), C.byref(stride)) == -1
+    assert lib.ffmp_ring_create(0, 4096, 1, None, 0, C.byref(ring), C.byref(base), C.byref(stride)) == -1
+    assert lib.ffmp_ring_create(0, 4096, 4, C.c_void_p(16), 0, C.byref(ring), C.byref(base), C.byref(stride)) == -1
+    rc = lib.ffmp_ring_create(0, 1 << 20, 4, None, 0, C.byref(ring), C.byref(base), C.byref(stride))
+    assert rc == -2 and not ring.value and b"ffmp_ring" in lib.ffmp_last_error()
+    assert lib.ffmp_ring_rebuild(None, 1, None, 0, C.byref(ring), C.byref(base), C.byref(stride)) == -1
     assert lib.ffmp_ring_destroy(None) == 0
     assert lib.ffmp_ring_pool_bytes(-1) == 0
+    info = (C.c_double * 5)()
+    assert lib.ffmp_ring_info(None, info, 5) == -1

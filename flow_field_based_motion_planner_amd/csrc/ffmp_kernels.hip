@@ -1129,6 +1129,14 @@ hipError_t map_rw(char* va, size_t bytes, hipMemGenericAllocationHandle_t h, int
   return hipMemSetAccess(va, bytes, &acc, 1);
 }
 
+// reservation alignment for pieces of `bytes`: the largest power of two <= min(bytes, 1 GiB),
+// at least the granularity (so every piece can map with the largest page fragments)
+size_t va_align(size_t bytes, size_t gran) {
+  size_t a = gran;
+  while (a * 2 <= bytes && a * 2 <= ((size_t)1 << 30)) a *= 2;
+  return a;
+}
+
 // a fresh piece mapped at its home address; on failure nothing stays allocated
 hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out) {
   hipMemAllocationProp prop = dev_prop(device);
@@ -1137,8 +1145,7 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
   p.device = device;
   hipError_t e = hipMemCreate(&p.h, bytes, &prop, 0);
   if (e != hipSuccess) return e;
-  if ((e = hipMemAddressReserve((void**)&p.home, bytes, std::max(gran, std::min(bytes, (size_t)1 << 30)), nullptr, 0)) !=
-      hipSuccess) {
+  if ((e = hipMemAddressReserve((void**)&p.home, bytes, va_align(bytes, gran), nullptr, 0)) != hipSuccess) {
     (void)hipMemRelease(p.h);  // never mapped: safe to give back
     return e;
   }
@@ -1223,6 +1230,10 @@ void pool_put(const std::vector<ffmp_piece>& v) {
   for (const ffmp_piece& p : v) g_pieces.push_back(p);
 }
 
+// a two-stream probe at or above this is a well-paired piece (MI355X: 6.7-7.0 TB/s paired
+// well, 4.5-5.6 badly; tools/pair_alias_probe.hip)
+constexpr double kPairFastGBs = 6200.0;
+
 // Pieces beyond the ones a ring needs (pairing candidates) only while the device keeps
 // max(8 GiB, 5 %) free beside them.
 bool room_for(size_t bytes) {
@@ -1267,6 +1278,7 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
   for (char n : need) todo += n != 0;
   const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
   double ref = 0.0;                          // best probe seen: the scale "fast" is judged against
+  bool found_fast = false;
   int fresh = 0;
   hipError_t e = hipSuccess;
   for (size_t pos = 0; pos < need.size(); ++pos) {
@@ -1275,7 +1287,9 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
     const size_t off = (size_t)j * g.piece;
     char* pb = g.pairing ? (char*)partner + off : nullptr;
     const size_t pbytes = g.pairing && (int64_t)off < partner_bytes ? std::min(g.piece, (size_t)(partner_bytes - (int64_t)off)) : 0;
-    const bool test = g.pairing && pbytes >= (64u << 20);
+    // no probe has found a fast pair in the first 12: the partner sits where nothing pairs
+    // well (seen at C5), so stop paying for probes and extra pieces
+    const bool test = g.pairing && pbytes >= (64u << 20) && (found_fast || r->pieces_tested < 12);
     int pick = -1, here = 0;
     double pick_gbs = -1.0;
     size_t k = 0;
@@ -1305,6 +1319,7 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
       const double gbs = pair_gbs(cand[c].home, pb, pbytes, s, e0, e1);
       ++r->pieces_tested;
       ++here;
+      if (gbs >= kPairFastGBs) found_fast = true;
       if (gbs > ref) ref = gbs;
       if (gbs > pick_gbs) {
         pick = c;
@@ -1333,8 +1348,7 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
 // reserve the ring's own addresses and map slots 0..W-1, then slot 0's pieces again
 int ring_map(ffmp_ring* r, const RingGeom& g) {
   // aligned to the piece (up to 1 GiB) so that every piece maps with the largest page fragments
-  hipError_t e = hipMemAddressReserve((void**)&r->va, r->vbytes, std::max(g.gran, std::min(g.piece, (size_t)1 << 30)),
-                                      nullptr, 0);
+  hipError_t e = hipMemAddressReserve((void**)&r->va, r->vbytes, va_align(g.piece, g.gran), nullptr, 0);
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipMemAddressReserve: %s", hipGetErrorString(e));
   for (int v = 0; v <= r->slots; ++v) {
     const int slot = v % r->slots;

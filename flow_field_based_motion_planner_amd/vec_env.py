@@ -342,7 +342,7 @@ class FFMPVec:
     # newest-only raster over two ring cycles and rebuild the ring with new pieces for slots
     # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.
     SLOW_SLOT = 1.06
-    REPAIR_ROUNDS = 2
+    REPAIR_ROUNDS = 1
 
     def _slot_ms(self) -> Dict[int, float]:
         """Median newest-only raster ms per physical slot written, over two ring cycles."""

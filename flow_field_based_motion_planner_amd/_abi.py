@@ -255,9 +255,9 @@ class SeamlessRing:
             return None, 0
         return partner.data_ptr(), partner.numel() * partner.element_size()
 
-    def _adopt(self, ring, base, stride) -> None:
-        """Wrap a fresh ring as the (slots + 1, *plane) tensor; this object keeps the creator's
-        reference (the handle) so the ring can be rebuilt."""
+    def _adopt(self, ring, base, stride, zero: bool = True) -> None:
+        """Wrap a fresh ring as the (slots + 1, *plane) tensor (zeroed unless `zero` is False);
+        this object keeps the creator's reference (the handle) so the ring can be rebuilt."""
         esize = self.bits // 8
         try:
             inner = [1]
@@ -266,7 +266,8 @@ class SeamlessRing:
             shape = (self.slots + 1,) + self.plane_shape
             strides = (stride.value // esize,) + tuple(inner)
             t = tensor_from_pointer(base.value, shape, strides, DL_ROCM, self.device_id, self.bits, owner=ring.value)
-            t[:self.slots].zero_()  # stream-ordered with the launches that follow
+            if zero:
+                t[:self.slots].zero_()  # stream-ordered with the launches that follow
         except Exception:
             self.lib.ffmp_ring_destroy(ring)
             raise
@@ -277,13 +278,14 @@ class SeamlessRing:
 
     def rebuild(self, slot_mask: int, partner=None) -> None:
         """Replace the pieces of the slots in slot_mask (ffmp_ring_rebuild); `tensor` becomes a new
-        tensor — views of the old one must not be used any more."""
+        tensor — views of the old one must not be used any more.  Kept slots keep their bytes,
+        replaced ones are undefined."""
         ring, base, stride = _P(), _P(), _I64()
         pp, pb = self._partner(partner)
         check(self.lib.ffmp_ring_rebuild(C.c_void_p(self.handle), int(slot_mask), pp, pb, C.byref(ring),
                                          C.byref(base), C.byref(stride)), "ffmp_ring_rebuild")
         self.rebuilds += 1
-        self._adopt(ring, base, stride)
+        self._adopt(ring, base, stride, zero=False)
 
     def info(self) -> dict:
         out = (C.c_double * 5)()

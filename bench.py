@@ -52,6 +52,8 @@ def parse():
                    help="frames per env kept in HBM (2 = contiguous (N,2,G,G) rewritten every step; default auto)")
     p.add_argument("--ring", default="auto", choices=["auto", "seamless", "wrap"],
                    help="frame ring with frame_window > 2: seamless (VMM alias, never wraps) or wrap")
+    p.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
+                   help="one-launch step (ffmp_step_fused) on/off, or auto: the instance's autotune decides")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -125,7 +127,7 @@ def cpu_baseline_parallel(cfg, seconds: float, procs: int):
                       f"1 thread per process"}
 
 
-def load_traffic(workload: str, n_envs: int, window: int, ring: str):
+def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if not os.path.exists(path):
@@ -134,7 +136,7 @@ def load_traffic(workload: str, n_envs: int, window: int, ring: str):
         with open(path) as f:
             d = json.load(f)
         if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window \
-                or d.get("ring", "wrap" if window > 2 else "contiguous") != ring:
+                or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused:
             return None
         return float(d["raster_hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
@@ -179,7 +181,8 @@ def main():
         strong = False
     n_total = n * world
     env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
-                  frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring])
+                  frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring],
+                  fused={"auto": None, "on": True, "off": False}[args.fused])
 
     K, W = args.steps, args.warmup
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -209,9 +212,11 @@ def main():
     env.check_errors()
     resets = int(env.episode.sum()) - ep0  # auto-resets in the timed steps
 
-    # raster kernel: HIP events around every launch on the launch stream; algorithmic bytes per
-    # launch from the frame-window schedule (full launches write both frames), plus the older
-    # frame of every env reset during a newest-only launch (resets spread evenly over launches)
+    # the dominant kernel — the raster, or with the one-launch step the fused env-step + raster
+    # kernel: HIP events around every launch on the launch stream; algorithmic bytes per launch
+    # from the frame-window schedule (full launches write both frames; the fused kernel adds the
+    # env step's state bytes), plus the older frame of every env reset during a newest-only
+    # launch (resets spread evenly over launches)
     r_ms = [r[0].elapsed_time(r[1]) for r in raster_ev]
     if args.dump_launches:
         print("raster ms per launch:", " ".join(f"{x:.3f}" for x in r_ms), file=sys.stderr, flush=True)
@@ -224,7 +229,7 @@ def main():
                            seamless=env.ring == "seamless")
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
     per_launch_envs = raster_ev[0][2]
-    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring)
+    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring, env.fused)
 
     if rank == 0:
         out = {
@@ -243,13 +248,13 @@ def main():
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow),
-                       "frame_window": env.frame_window, "ring": env.ring,
+                       "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
-                         "kernel": "raster_kernel", "kernel_ms": raster_ms,
+                         "kernel": "step_raster_kernel" if env.fused else "raster_kernel", "kernel_ms": raster_ms,
                          "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
                          "launches_per_step": len(r_ms) // K, "full_launches": n_full,
                          "timed_resets": resets},

@@ -149,29 +149,16 @@ FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const Fra
 // float64 work (integrator, trig, goal, reward, record header) is issued once per 64/LPE envs
 // instead of once per env; lane k of an env's group holds its obstacle k, beams and footprint
 // cells are strided over the group's lanes.
-template <int MODE, int kEnvWaves, int LPE>
-__global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
-                                                 const int64_t* __restrict__ action,
-                                                 const uint8_t* __restrict__ mask, int32_t initial,
-                                                 ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
+// One env's step (or reset) by its LPE-lane group: lane = the lane within the group, s_* = the
+// group's LDS slices (FFMP_MAX_OBST entries each).  Used by env_kernel and step_raster_kernel.
+template <int MODE, int LPE>
+FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, int64_t env_offset,
+                                                       const int64_t* __restrict__ action, int32_t initial,
+                                                       const ffmp_state_t& st, const ffmp_obs_t& ob,
+                                                       const ffmp_out_t& out, int64_t e, int lane, double* s_ox,
+                                                       double* s_oy, double* s_or, float4* s_ecur,
+                                                       float4* s_eprev) {
   static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
-  constexpr int EPW = 64 / LPE;  // envs per wave
-  __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
-      s_ora[kEnvWaves][FFMP_MAX_OBST];
-  __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
-
-  const int wv = threadIdx.x >> 6;
-  const int grp = (threadIdx.x & 63) / LPE;
-  const int64_t e = ((int64_t)blockIdx.x * kEnvWaves + wv) * EPW + grp;
-  const int lane = threadIdx.x & (LPE - 1);  // lane within the env's group
-  double* s_ox = s_oxa[wv] + grp * LPE;
-  double* s_oy = s_oya[wv] + grp * LPE;
-  double* s_or = s_ora[wv] + grp * LPE;
-  float4* s_ecur = s_ecura[wv] + grp * LPE;
-  float4* s_eprev = s_epreva[wv] + grp * LPE;
-  if (e >= n) return;
-  if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
-
   const int K = cfg.n_obst;
   const int L = cfg.n_beams;
   const int G = cfg.grid;
@@ -365,6 +352,27 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
   }
 }
 
+template <int MODE, int kEnvWaves, int LPE>
+__global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+                                                 const int64_t* __restrict__ action,
+                                                 const uint8_t* __restrict__ mask, int32_t initial,
+                                                 ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
+  constexpr int EPW = 64 / LPE;  // envs per wave
+  __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
+      s_ora[kEnvWaves][FFMP_MAX_OBST];
+  __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
+
+  const int wv = threadIdx.x >> 6;
+  const int grp = (threadIdx.x & 63) / LPE;
+  const int64_t e = ((int64_t)blockIdx.x * kEnvWaves + wv) * EPW + grp;
+  const int lane = threadIdx.x & (LPE - 1);  // lane within the env's group
+  if (e >= n) return;
+  if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
+  env_group<MODE, LPE>(cfg, env_offset, action, initial, st, ob, out, e, lane, s_oxa[wv] + grp * LPE,
+                       s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_ecura[wv] + grp * LPE,
+                       s_epreva[wv] + grp * LPE);
+}
+
 // ============================================================================
 // raster_kernel: the HBM-bound hot path.
 //   block = 256 threads (4 waves); a pass covers 1024 consecutive cells of one
@@ -405,32 +413,29 @@ FFMP_DEV int small_div(int r, float invG) { return (int)(((float)r + 0.5f) * inv
 
 }  // namespace
 
-template <bool NT, bool XCD, bool FLOW>
-__global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
-                                                     int32_t cells_per_block,
-                                                     const float* __restrict__ record,
-                                                     const uint8_t* __restrict__ mask,
-                                                     float* __restrict__ state_m, int64_t sm_stride,
-                                                     int64_t sm_frame, int32_t newest_only,
-                                                     float* __restrict__ pot,
-                                                     float* __restrict__ flow, int32_t tile_log2r) {
-  __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
-  __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
-  __shared__ float s_hdr[FFMP_REC_HDR];
-
-  // XCD-aware remap: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one), so
-  // logical block (b % 8) * per + b / 8 gives every XCD a contiguous range of (env, tile)
-  // work: 8x less concurrently written footprint per XCD.  A placement-only change.
+// XCD-aware remap: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one), so
+// logical block (b % 8) * per + b / 8 gives every XCD a contiguous range of (env, tile) work:
+// 8x less concurrently written footprint per XCD.  A placement-only change.
+template <bool XCD>
+FFMP_DEV int64_t logical_block() {
   int64_t lb = blockIdx.x;
   if (XCD) {
     const int64_t per = (int64_t)gridDim.x / 8;
     if (lb < per * 8) lb = (lb % 8) * per + lb / 8;
   }
-  const int64_t e = lb / bpe;
-  const int tile = (int)(lb - e * bpe);
-  if (e >= n) return;
-  if (mask && !mask[e]) return;
+  return lb;
+}
 
+// The raster of cells [tile * cells_per_block, ...) of env e by the whole 256-thread block
+// (block-uniform arguments; contains a block barrier).
+template <bool NT, bool FLOW>
+FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, int64_t e, int tile, int32_t cells_per_block,
+                                                        const float* __restrict__ record,
+                                                        float* __restrict__ state_m, int64_t sm_stride,
+                                                        int64_t sm_frame, int32_t newest_only,
+                                                        float* __restrict__ pot, float* __restrict__ flow,
+                                                        int32_t tile_log2r, float4* s_cur, float4* s_prev,
+                                                        float2* s_vel, float* s_hdr) {
   const int K = cfg.n_obst;
   const int G = cfg.grid;
   const int G2 = G * G;
@@ -572,6 +577,54 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
       task(i0, i1, j0, j1, i0 + di, off - di * G, q, q < qend);
     }
   }
+}
+
+template <bool NT, bool XCD, bool FLOW>
+__global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
+                                                     int32_t cells_per_block,
+                                                     const float* __restrict__ record,
+                                                     const uint8_t* __restrict__ mask,
+                                                     float* __restrict__ state_m, int64_t sm_stride,
+                                                     int64_t sm_frame, int32_t newest_only,
+                                                     float* __restrict__ pot,
+                                                     float* __restrict__ flow, int32_t tile_log2r) {
+  __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
+  __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
+  __shared__ float s_hdr[FFMP_REC_HDR];
+  const int64_t lb = logical_block<XCD>();
+  const int64_t e = lb / bpe;
+  const int tile = (int)(lb - e * bpe);
+  if (e >= n) return;
+  if (mask && !mask[e]) return;
+  raster_env<NT, FLOW>(cfg, e, tile, cells_per_block, record, state_m, sm_stride, sm_frame, newest_only, pot, flow,
+                       tile_log2r, s_cur, s_prev, s_vel, s_hdr);
+}
+
+// The fused step: one block per env.  Wave 0 steps the env (env_group, 64 lanes: integrator,
+// obstacles, lidar, collision / reward / done, auto-reset, record), then the block rasters the
+// env's whole plane from the record it just wrote.  The env step's float64 work of one block
+// overlaps the store streams of the other blocks on the CU, instead of running as its own
+// launch before the raster (~4 % of a C3 step).
+template <bool NT, bool XCD, bool FLOW>
+__global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+                                                          const int64_t* __restrict__ action, ffmp_state_t st,
+                                                          ffmp_obs_t ob, ffmp_out_t out, int64_t sm_stride,
+                                                          int64_t sm_frame, int32_t newest_only,
+                                                          int32_t tile_log2r) {
+  __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST];
+  __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
+  __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
+  __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
+  __shared__ float s_hdr[FFMP_REC_HDR];
+  const int64_t e = logical_block<XCD>();
+  if (e >= n) return;
+  if (threadIdx.x < 64)
+    env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
+                                 s_ecur, s_eprev);
+  __threadfence_block();  // the record (global) is read by every wave below
+  __syncthreads();
+  raster_env<NT, FLOW>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
+                       ob.potential, ob.flow, tile_log2r, s_cur, s_prev, s_vel, s_hdr);
 }
 
 // ============================================================================
@@ -965,6 +1018,57 @@ int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_
   int rc = ffmp_step_state(cfg, n, env_offset, action, state, obs, out, stream);
   if (rc) return rc;
   return ffmp_raster(cfg, n, state->record, nullptr, obs, stream);
+}
+
+int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,
+                    ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, int32_t flags, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0 || env_offset < 0) return fail(FFMP_E_ARG, "negative n or env_offset");
+  if (!state || !obs || !action || !out) return fail(FFMP_E_ARG, "state/obs/action/out is NULL");
+  if (!state->pose || !state->goal || !state->d0 || !state->t || !state->episode || !state->record || !state->err)
+    return fail(FFMP_E_ARG, "a state pointer is NULL");
+  if (cfg->n_obst > 0 && (!state->obst || !state->obst_r)) return fail(FFMP_E_ARG, "obstacle state NULL");
+  if (!obs->state_m || !obs->state_g || !obs->state_v || !obs->state_t || !obs->grad)
+    return fail(FFMP_E_ARG, "an obs pointer is NULL");
+  if (cfg->n_beams > 0 && !obs->lidar) return fail(FFMP_E_ARG, "obs.lidar NULL with n_beams > 0");
+  if (!out->reward || !out->done || !out->is_goal || !out->collide || !out->truncated)
+    return fail(FFMP_E_ARG, "an out pointer is NULL");
+  if ((flags & FFMP_RASTER_NT) && (flags & FFMP_RASTER_PLAIN)) return fail(FFMP_E_ARG, "NT and PLAIN both set");
+  const bool fl = cfg->flow != 0;
+  if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
+  if (n == 0) return FFMP_OK;
+  if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
+  const int G2 = cfg->grid * cfg->grid;
+  const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
+  const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
+  if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
+    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld floats (G*G = %d)", (long long)sm_stride,
+                (long long)sm_frame, G2);
+  const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
+  const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
+  const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
+  int32_t tile_log2r = (flags & FFMP_RASTER_TILE8) ? 3 : (flags & FFMP_RASTER_TILE4) ? 2 : (flags & FFMP_RASTER_TILE2) ? 1 : 0;
+  if (tile_log2r && (cfg->grid % (256 >> tile_log2r)) != 0) tile_log2r = 0;  // a block is one whole plane
+  const dim3 grid((unsigned)n), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  ffmp_out_t o = *out;
+#define FFMP_FUSED_LAUNCH(NT_, XCD_, FL_)                                                                     \
+  hipLaunchKernelGGL((step_raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, env_offset, action, *state, \
+                     *obs, o, sm_stride, sm_frame, newest, tile_log2r)
+  const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
+  switch (sel) {
+    case 0: FFMP_FUSED_LAUNCH(false, false, false); break;
+    case 1: FFMP_FUSED_LAUNCH(false, false, true); break;
+    case 2: FFMP_FUSED_LAUNCH(false, true, false); break;
+    case 3: FFMP_FUSED_LAUNCH(false, true, true); break;
+    case 4: FFMP_FUSED_LAUNCH(true, false, false); break;
+    case 5: FFMP_FUSED_LAUNCH(true, false, true); break;
+    case 6: FFMP_FUSED_LAUNCH(true, true, false); break;
+    default: FFMP_FUSED_LAUNCH(true, true, true); break;
+  }
+#undef FFMP_FUSED_LAUNCH
+  return check_launch("ffmp_step_fused");
 }
 
 int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n, const double* scan, int32_t scan_len,

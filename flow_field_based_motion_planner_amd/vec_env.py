@@ -64,13 +64,17 @@ class FFMPVec:
             wraps and every step writes only the new frame; `frames` is (W+1, N, G, G) with
             frames[W] aliasing frames[0].  None (default): seamless when the device supports
             it, else the wrapping ring.  False: always the wrapping ring.
+        fused: True: every step is ONE launch (ffmp_step_fused: one block per env steps the env,
+            then rasters its plane); False: the env kernel, then the raster; None (default): the
+            autotune times both on this instance and keeps the faster (small batches: False).
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
                  device: Optional[Union[str, torch.device]] = None, env_offset: int = 0,
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
-                 frame_window: Optional[int] = None, seamless: Optional[bool] = None):
+                 frame_window: Optional[int] = None, seamless: Optional[bool] = None,
+                 fused: Optional[bool] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -100,6 +104,9 @@ class FFMPVec:
             raise ValueError("seamless=True needs frame_window > 2")
         self.ring = "contiguous" if self.frame_window == 2 else "wrap"  # or "seamless" (set by _alloc)
         self.ring_meta = None
+        self.fused = bool(fused) if fused is not None else False  # autotune may switch it on
+        self._fused_req = fused
+        self.fused_flags = _abi.RASTER_NT
         self._wpos = 0  # frame slot of state_m[:, 0]
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
@@ -108,6 +115,10 @@ class FFMPVec:
         self.pipeline_slices = max(1, min(int(pipeline), self.num_envs))
         if self.pipeline_slices > 1 and self.frame_window != 2:
             raise ValueError("pipeline > 1 needs frame_window=2")
+        if self.pipeline_slices > 1 and fused:
+            raise ValueError("pipeline > 1 and fused=True are exclusive")
+        if self.pipeline_slices > 1:
+            self._fused_req = False
         self._build_structs()
         plane_bytes = self._nbytes((self.num_envs, (3 if potential else 2) + (2 if self.cfg.flow else 0), G2),
                                    torch.float32)
@@ -280,8 +291,11 @@ class FFMPVec:
         a = torch.full((self.num_envs,), 10, dtype=torch.int64, device=self.device)
         self.step(a)
         t = []
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
         for _ in range(steps):
             self.step(a, timing=t)
+        ev[1].record()
         torch.cuda.synchronize(self.device)
         out = {}
         for full in (True, False):
@@ -289,6 +303,7 @@ class FFMPVec:
             if sel:
                 ms = sum(r[0].elapsed_time(r[1]) for r in sel)
                 out[full] = (sum(r[3] for r in sel) / (ms * 1e-3) / 1e9, ms / len(sel))
+        out["step_ms"] = ev[0].elapsed_time(ev[1]) / steps
         return out
 
     # Placement retries.  Two planes written in lockstep (a frame slot and the potential plane)
@@ -422,13 +437,43 @@ class FFMPVec:
             self.raster_shape = best[False][2]
         self.raster_shape_newest = best[False][2] if False in best else self.raster_shape
         gbs = self._cycle_gbs(best[True][1] if True in best else None, best[False][1] if False in best else None)
+        fused = self._tune_fused(steps)
         self.placement = {"shape": {"cells_per_block": self.raster_shape[0], "flags": self.raster_shape[1]},
                           "shape_newest": ({"cells_per_block": self.raster_shape_newest[0],
                                             "flags": self.raster_shape_newest[1]} if False in best else None),
                           "gbs": round(gbs, 1),
                           "candidates": [[c, f] + [round(r[k][0], 1) for k in (True, False) if k in r]
-                                         for r, (c, f) in results]}
+                                         for r, (c, f) in results],
+                          "fused": fused}
         self._clear_after_tuning()
+
+    # Fused-step candidates (ffmp_step_fused flags; a block is a whole plane, so no cells/block)
+    FUSED_FLAGS = (
+        _abi.RASTER_NT, _abi.RASTER_PLAIN, _abi.RASTER_NT | _abi.RASTER_XCD, _abi.RASTER_PLAIN | _abi.RASTER_XCD,
+        _abi.RASTER_NT | _abi.RASTER_TILE4, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4,
+        _abi.RASTER_PLAIN | _abi.RASTER_TILE4, _abi.RASTER_NT | _abi.RASTER_TILE2,
+        _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE2, _abi.RASTER_NT | _abi.RASTER_TILE8,
+    )
+
+    def _tune_fused(self, steps: int) -> Optional[dict]:
+        """Time whole steps of the two-launch path (the tuned raster shapes) against the fused
+        step for each FUSED_FLAGS candidate; keep the faster (fused=None), or the best fused flags
+        (fused=True)."""
+        if self._fused_req is False or self.pipeline_slices > 1:
+            self.fused = False
+            return None
+        self.fused = False
+        sep = self._raster_gbs_steady(steps)["step_ms"]
+        self.fused = True
+        res = []
+        for f in self.FUSED_FLAGS:
+            self.fused_flags = f
+            res.append((self._raster_gbs_steady(steps)["step_ms"], f))
+        best_ms, best_f = min(res)
+        self.fused_flags = best_f
+        self.fused = bool(self._fused_req) or best_ms < 0.995 * sep
+        return {"chosen": self.fused, "two_launch_step_ms": round(sep, 4), "fused_step_ms": round(best_ms, 4),
+                "flags": best_f, "candidates": [[f, round(m, 4)] for m, f in res]}
 
     def _placement_gbs(self) -> float:
         """Cycle bandwidth of the current buffers with the current launch shapes."""
@@ -584,9 +629,9 @@ class FFMPVec:
         m = None if mask is None else mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
         self._raster_launch(True, m)
 
-    def raster_step(self, timing: Optional[list] = None) -> None:
-        """Kernel 2 of a step (the HBM-bound hot kernel): slide the frame pair by one and raster
-        the new frame + potential (+ flow), or both frames when the window wraps or W == 2."""
+    def _next_window(self) -> bool:
+        """Slide the [older, newest] pair by one slot for the next raster; True if that raster
+        must write both frames (the wrapping ring's wrap, or W = 2)."""
         p = self._wpos + 1
         if self.ring == "seamless":  # virtual slot W is slot 0: the pair slides forever
             full = False
@@ -594,6 +639,35 @@ class FFMPVec:
         else:
             full = p > self.frame_window - 2
         self._set_window(0 if full else p)
+        return full
+
+    def _state_bytes(self, n: int) -> int:
+        """Algorithmic bytes of the env step itself over n envs (state read + write, small obs,
+        lidar, record write, action, reward and flags; config.bytes_per_env_step "state")."""
+        from .config import bytes_per_env_step
+        return n * bytes_per_env_step(self.cfg, potential=self.potential is not None)["state"]
+
+    def _step_fused(self, actions, timing: Optional[list] = None) -> None:
+        """Env step + raster in one launch (ffmp_step_fused): one block per env."""
+        a = self._actions(actions)
+        self._act_keepalive = a
+        full = self._next_window()
+        flags = self.fused_flags | (0 if full else _abi.RASTER_NEWEST)
+        if timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _abi.check(self.lib.ffmp_step_fused(C.byref(self._cfg_c), self.num_envs, self.env_offset, a.data_ptr(),
+                                            C.byref(self._state_c), C.byref(self._obs_c), C.byref(self._out_c), flags,
+                                            self._stream()), "ffmp_step_fused")
+        if timing is not None:
+            e1.record()
+            n = self.num_envs
+            timing.append((e0, e1, n, self._raster_bytes(n, full) + self._state_bytes(n), full))
+
+    def raster_step(self, timing: Optional[list] = None) -> None:
+        """Kernel 2 of a step (the HBM-bound hot kernel): slide the frame pair by one and raster
+        the new frame + potential (+ flow), or both frames when the window wraps or W == 2."""
+        full = self._next_window()
         self._raster_launch(full, None, timing)
 
     def _step_pipelined(self, actions, timing) -> None:
@@ -632,6 +706,8 @@ class FFMPVec:
         with torch.cuda.device(self.device):
             if self.pipeline_slices > 1:
                 self._step_pipelined(actions, timing)
+            elif self.fused:
+                self._step_fused(actions, timing)
             else:
                 self.step_state(actions)
                 self.raster_step(timing)

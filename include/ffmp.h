@@ -214,6 +214,14 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                    const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
                    int32_t flags, void* stream);
 
+/* ffmp_step_state + ffmp_raster_ex in ONE launch (same results): one block per env, whose first
+ * wave steps the env and whose 4 waves then raster its whole plane from the record just written
+ * (flags as ffmp_raster_ex; cells_per_block is the whole plane, so TILE* needs only
+ * G % (256/R) == 0).  The env step's float64 work overlaps other blocks' store streams instead
+ * of running as its own launch. */
+int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,
+                    ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, int32_t flags, void* stream);
+
 /* ffmp_step_state + ffmp_raster. */
 int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
               const int64_t* action, ffmp_state_t* state, ffmp_obs_t* obs,

@@ -30,9 +30,11 @@ CASES = {
 }
 
 
-def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True, frame_window=None):
+def _run(cfg, n, steps, seed=0, env_offset=0, keep_terminal=True, frame_window=None, fused=None, fused_flags=None):
     env = FFMPVec(n, cfg, device="cuda:0", env_offset=env_offset, keep_terminal=keep_terminal,
-                  frame_window=frame_window)
+                  frame_window=frame_window, fused=fused)
+    if fused_flags is not None:
+        env.fused_flags = fused_flags
     ref = OracleVecEnv(cfg, n, env_offset=env_offset)
     env.reset()
     ref.reset()
@@ -64,6 +66,46 @@ def test_step_parity(name):
     assert not problems, "\n".join(problems[:20])
     if name == "dense_collisions":
         assert counts["collision"] > 0 and counts["done"] > 0, counts  # the reset path is exercised
+
+
+@pytest.mark.parametrize("name", ["C1_64_static", "C3_256_moving_lidar", "dense_collisions", "flow_planes",
+                                  "G100_reference_map", "no_obstacles"])
+def test_fused_step_parity(name):
+    """The one-launch step (ffmp_step_fused: env step by wave 0, then the block's raster) against
+    the oracle, through the seamless ring, with the 2-D tiles where the grid allows them."""
+    from flow_field_based_motion_planner_amd import _abi
+    cfg, n, steps = CASES[name]
+    flags = _abi.RASTER_NT | _abi.RASTER_TILE4 | (_abi.RASTER_XCD if n >= 16 else 0)
+    env, ref, problems, counts = _run(cfg, n, steps, frame_window=4, fused=True, fused_flags=flags)
+    assert env.fused
+    assert not problems, "\n".join(problems[:20])
+    if name == "dense_collisions":
+        assert counts["collision"] > 0 and counts["done"] > 0, counts
+
+
+def test_fused_equals_two_launch_every_flag():
+    """Every fused flag set writes the same planes and outputs as the two-launch step."""
+    cfg = FFMPConfig(grid=128, n_obst=24, n_beams=40, moving=True, obst_rmax=0.7, obst_vmax=1.5, flow=True,
+                     world_half=5.0, max_steps=5, seed=12)
+    n = 21
+    ref_env = FFMPVec(n, cfg, device="cuda:0", frame_window=3, fused=False)
+    ref_env.reset()
+    gen = torch.Generator(device="cuda:0").manual_seed(4)
+    acts = torch.randint(0, 28, (8, n), device="cuda:0", generator=gen)
+    want = []
+    for k in range(8):
+        o, r, d, _ = ref_env.step(acts[k], copy=True)
+        want.append((o, r, d))
+    for flags in FFMPVec.FUSED_FLAGS:
+        env = FFMPVec(n, cfg, device="cuda:0", frame_window=3, fused=True)
+        env.fused_flags = flags
+        env.reset()
+        for k in range(8):
+            o, r, d, _ = env.step(acts[k])
+            wo, wr, wd = want[k]
+            assert torch.equal(d, wd) and torch.equal(r, wr), (flags, k)
+            for key in ("state_m", "potential", "flow", "lidar", "state_g", "state_v", "grad"):
+                assert torch.equal(o[key], wo[key]), (flags, k, key)
 
 
 def test_truncation_and_autoreset_counts():

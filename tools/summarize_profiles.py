@@ -44,6 +44,7 @@ def counters(path, name):
                       key=lambda r: int(r["Dispatch_Id"]))
     for row in rows:
         k = row["Kernel_Name"]
+        # "raster_kernel" = the timed kernel: raster_kernel or step_raster_kernel (fused step)
         key = "raster_kernel" if "raster_kernel" in k else ("env_kernel" if "env_kernel" in k else k)
         per.setdefault(key, []).append(float(row["Counter_Value"]))
     return per
@@ -90,12 +91,14 @@ def main():
         pm["n_envs"] = n
         pm["frame_window"] = bj["config"].get("frame_window", 2)
         pm["ring"] = bj["config"].get("ring", "wrap" if pm["frame_window"] > 2 else "contiguous")
+        pm["fused"] = bool(bj["config"].get("fused", False))
+        pm["timed_kernel"] = bj["roofline"].get("kernel", "raster_kernel")
         pm["raster_algorithmic_bytes_per_launch"] = alg
         if "raster_kernel" in pm["kernels"]:
             hb = pm["kernels"]["raster_kernel"]["hbm_bytes"]
             pm["raster_traffic_over_algorithmic"] = hb / alg
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
-                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"],
+                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
                            "raster_hbm_bytes_per_launch": hb,
                            "source": f"{tag}_{cfg}_pmc.json"}, f, indent=1)
     trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")

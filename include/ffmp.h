@@ -15,9 +15,11 @@
  *                          src/train.py:532-566 (start/goal, temporal stack
  *                          duplication, velocity := 0, d0 := dist) and the
  *                          commented-out FFMP.reset src/gym_ffmp/envs/ffmp.py:77-83
- *   ffmp_step           -> one iteration of src/train.py:523-693 with Gazebo
+ *   ffmp_step, ffmp_step_fused -> one iteration of src/train.py:523-693 with Gazebo
  *                          (/cmd_vel integration), /bev_* rasterisers and
  *                          rewarder2 (src/gym_ffmp/envs/ffmp.py:179-188) in-GPU
+ *   ffmp_ring_*, ffmp_dlpack -> storage of make_temporal_maps' 2-frame stack
+ *                          (src/train.py:474-486) kept in place (optional helper)
  *   ffmp_raster         -> external /bev_flow_estimator + /temporal_bev_publisher
  *                          (src/train.py:116-121, make_temporal_maps :474-486)
  *   ffmp_reward_done    -> FFMP.rewarder / rewarder2 / reward_calculator /

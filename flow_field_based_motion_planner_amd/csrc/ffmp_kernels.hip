@@ -10,7 +10,9 @@
 //                      writes the two float32 occupancy frames of state_m and
 //                      the float32 potential plane with 16-B stores; obstacles
 //                      staged in LDS and culled per 256-cell wave chunk.
+//   step_raster_kernel the one-launch step: one block per env, env step then raster.
 //   reward_done_kernel / footprint_kernel / scan_kernel — legacy FFMP methods.
+// The seamless frame ring (HIP virtual memory) and the DLPack hand-off: ffmp_ring.hip.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -19,19 +21,14 @@
 #include <stddef.h>
 #include <string.h>
 
-#include <algorithm>
-#include <memory>
-#include <mutex>
-#include <vector>
-
 #include "ffmp_device.h"
 
 #pragma clang fp contract(off)
 
 using namespace ffmp;
 
-namespace {
-
+// The thread-local error message behind ffmp_last_error(), shared with ffmp_ring.hip.
+namespace ffmp_detail {
 thread_local char g_err[512] = "";
 
 __attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
@@ -41,6 +38,11 @@ __attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
   va_end(ap);
   return code;
 }
+}  // namespace ffmp_detail
+using ffmp_detail::fail;
+using ffmp_detail::g_err;
+
+namespace {
 
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -1135,473 +1137,6 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
   hipLaunchKernelGGL(episode_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      n, *out, window, max_steps, threshold, flags, *ep);
   return check_launch("ffmp_episode_update");
-}
-
-}  // extern "C"
-
-// ------------------------------------------------------------------ seamless frame ring
-// Built from physical PIECES (hipMemCreate handles of piece_bytes): slot i of the ring is n
-// pieces mapped back to back, and virtual slot W maps slot 0's pieces a second time (the
-// alias).  Two findings on MI355X / ROCm 7.2 shape it:
-//
-// * Pairing.  The raster writes a frame slot and the potential plane in lockstep (same offset,
-//   same time).  Two lockstep store streams run at ~6.9 TB/s or at 4.6-5.6 TB/s depending on
-//   the PHYSICAL memory each lands in (tools/pair_alias_probe.hip: two virtual mappings of the
-//   same pages pair identically; tools/region_probe.hip), so one slot that pairs badly with
-//   the potential plane makes one step in W ~25 % slower.  With a `partner` (the potential
-//   plane), every piece position (slot i, piece j) gets a piece measured to pair well with the
-//   partner's bytes [j*P, (j+1)*P): a two-stream store probe, candidates from the free-piece
-//   pool first, then fresh pieces; pieces that pair badly here stay pooled for other positions
-//   or later rings.
-// * Never unmap.  Once a VMM range is unmapped and its address reused by a new mapping, the
-//   runtime can still resolve the address to the OLD allocation (tools/ring_reuse_probe.hip:
-//   D2H copies of a fresh mapping return the previous ring's bytes; FFMPVec saw the first
-//   raster into a fresh ring vanish).  So nothing is ever unmapped before exit: every piece
-//   keeps a private "home" mapping, a ring maps its pieces once more at a fresh address, and a
-//   ring whose last reference is dropped returns its pieces to the pool (its addresses are
-//   simply never used again).
-struct ffmp_piece {
-  hipMemGenericAllocationHandle_t h;
-  char* home;  // private mapping, for the pairing probe
-  size_t bytes;
-  int32_t device;
-};
-
-struct ffmp_ring {
-  int32_t device;
-  int32_t slots;
-  size_t stride;  // slot stride = pieces_per_slot * piece bytes
-  char* va;
-  size_t vbytes;
-  int refs;  // the creator + one per live DLPack tensor (atomic)
-  std::vector<ffmp_piece> pieces;  // slot-major, slots * pieces_per_slot
-  double pair_gbs_min, pair_gbs_max;  // pairing probe of the chosen pieces (0 without partner)
-  int pieces_new, pieces_tested;
-};
-
-// dlpack.h (v0.8) DLManagedTensor, the interchange torch.utils.dlpack.from_dlpack consumes
-struct DLDevice_ { int32_t device_type, device_id; };
-struct DLDataType_ { uint8_t code, bits; uint16_t lanes; };
-struct DLTensor_ {
-  void* data;
-  DLDevice_ device;
-  int32_t ndim;
-  DLDataType_ dtype;
-  int64_t* shape;
-  int64_t* strides;
-  uint64_t byte_offset;
-};
-struct DLManagedTensor_ {
-  DLTensor_ dl_tensor;
-  void* manager_ctx;
-  void (*deleter)(DLManagedTensor_*);
-};
-struct DLHolder_ {  // one allocation: the managed tensor, its shape/strides, its owner
-  DLManagedTensor_ mt;
-  int64_t dims[16];
-  ffmp_ring* owner;
-};
-
-// two lockstep 16-B nontemporal store streams over n16 float4s: the raster's write pattern
-__global__ __launch_bounds__(256) void pair_probe_kernel(f32x4* __restrict__ a, f32x4* __restrict__ b, int64_t n16) {
-  for (int64_t i = (int64_t)blockIdx.x * 4096 + threadIdx.x; i < n16 && i < ((int64_t)blockIdx.x + 1) * 4096; i += 256) {
-    const f32x4 x = {0.f, 1.f, 2.f, 3.f};
-    __builtin_nontemporal_store(x, a + i);
-    __builtin_nontemporal_store(x, b + i);
-  }
-}
-
-namespace {
-
-std::mutex g_pool_mu;
-std::vector<ffmp_piece> g_pieces;  // free pieces (mapped at home), reusable
-
-hipMemAllocationProp dev_prop(int32_t device) {
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = device;
-  return prop;
-}
-
-hipError_t map_rw(char* va, size_t bytes, hipMemGenericAllocationHandle_t h, int32_t device) {
-  hipError_t e = hipMemMap(va, bytes, 0, h, 0);
-  if (e != hipSuccess) return e;
-  hipMemAccessDesc acc = {};
-  acc.location = dev_prop(device).location;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  return hipMemSetAccess(va, bytes, &acc, 1);
-}
-
-// reservation alignment for pieces of `bytes`: the largest power of two <= min(bytes, 1 GiB),
-// at least the granularity (so every piece can map with the largest page fragments)
-size_t va_align(size_t bytes, size_t gran) {
-  size_t a = gran;
-  while (a * 2 <= bytes && a * 2 <= ((size_t)1 << 30)) a *= 2;
-  return a;
-}
-
-// a fresh piece mapped at its home address; on failure nothing stays allocated
-hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out) {
-  hipMemAllocationProp prop = dev_prop(device);
-  ffmp_piece p = {};
-  p.bytes = bytes;
-  p.device = device;
-  hipError_t e = hipMemCreate(&p.h, bytes, &prop, 0);
-  if (e != hipSuccess) return e;
-  if ((e = hipMemAddressReserve((void**)&p.home, bytes, va_align(bytes, gran), nullptr, 0)) != hipSuccess) {
-    (void)hipMemRelease(p.h);  // never mapped: safe to give back
-    return e;
-  }
-  if ((e = map_rw(p.home, bytes, p.h, device)) != hipSuccess) {
-    (void)hipMemUnmap(p.home, bytes);
-    (void)hipMemAddressFree(p.home, bytes);
-    (void)hipMemRelease(p.h);
-    return e;
-  }
-  *out = p;
-  return hipSuccess;
-}
-
-// GB/s of the two-stream store probe over `bytes` of piece home + partner range
-double pair_gbs(char* a, char* b, size_t bytes, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  const int64_t n16 = (int64_t)(bytes / 16);
-  const unsigned blocks = (unsigned)((n16 + 4095) / 4096);
-  float best = 1e30f;
-  for (int r = 0; r < 4; ++r) {
-    (void)hipEventRecord(e0, s);
-    hipLaunchKernelGGL(pair_probe_kernel, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
-    (void)hipEventRecord(e1, s);
-    if (hipEventSynchronize(e1) != hipSuccess) return 0.0;
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    if (r > 0 && ms < best) best = ms;  // first launch warms up
-  }
-  return 2.0 * (double)(n16 * 16) / (best * 1e-3) / 1e9;
-}
-
-void ring_unref(ffmp_ring* r) {
-  if (__atomic_sub_fetch(&r->refs, 1, __ATOMIC_ACQ_REL) > 0) return;
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (const ffmp_piece& p : r->pieces) g_pieces.push_back(p);  // the ring's addresses are retired
-  delete r;
-}
-
-// restores the caller's current device on scope exit
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int d) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != d) (void)hipSetDevice(d);
-  }
-  ~DeviceScope() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
-}  // namespace
-
-extern "C" {
-
-}  // extern "C"
-
-namespace {
-
-struct RingGeom {
-  size_t gran, piece, stride;
-  int per_slot;
-  bool pairing;
-};
-
-int ring_geom(int32_t device, int64_t slot_bytes, const void* partner, RingGeom* g) {
-  int vmm = 0;
-  if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
-    return fail(FFMP_E_HIP, "ffmp_ring: device %d has no virtual memory management", device);
-  hipMemAllocationProp prop = dev_prop(device);
-  hipError_t e = hipMemGetAllocationGranularity(&g->gran, &prop, hipMemAllocationGranularityMinimum);
-  if (e != hipSuccess || g->gran == 0) return fail(FFMP_E_HIP, "hipMemGetAllocationGranularity: %s", hipGetErrorString(e));
-  // pieces: 1 GiB for slots of >= 2 GiB (the pairing resolution), else one piece per slot
-  const size_t slot_g = ((size_t)slot_bytes + g->gran - 1) / g->gran * g->gran;
-  g->piece = slot_g >= (2ull << 30) ? (1ull << 30) : slot_g;
-  g->per_slot = (int)((slot_g + g->piece - 1) / g->piece);
-  g->stride = g->piece * (size_t)g->per_slot;
-  g->pairing = partner != nullptr && g->piece >= (256ull << 20);
-  return FFMP_OK;
-}
-
-void pool_put(const std::vector<ffmp_piece>& v) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (const ffmp_piece& p : v) g_pieces.push_back(p);
-}
-
-// a two-stream probe at or above this is a well-paired piece (MI355X: 6.7-7.0 TB/s paired
-// well, 4.5-5.6 badly; tools/pair_alias_probe.hip)
-constexpr double kPairFastGBs = 6200.0;
-
-// Pieces beyond the ones a ring needs (pairing candidates) only while the device keeps
-// max(8 GiB, 5 %) free beside them.
-bool room_for(size_t bytes) {
-  size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
-  const size_t reserve = std::max((size_t)8 << 30, total_b / 20);
-  return free_b > bytes + reserve;
-}
-
-// Fill r->pieces[pos] for every pos with need[pos] set: candidates from the pool first (at most
-// 6 per position), then fresh pieces; with a partner, the first piece whose two-stream store
-// probe against the partner bytes at the same offset is within 7 % of the best probe seen
-// (after >= 3 probes), else the best of 12.  `avoid` pieces are not candidates (they go to the
-// pool afterwards).
-int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
-                  int64_t partner_bytes, const std::vector<ffmp_piece>& avoid) {
-  const int32_t device = r->device;
-  std::vector<ffmp_piece> cand;
-  {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (size_t k = 0; k < g_pieces.size();) {
-      if (g_pieces[k].device == device && g_pieces[k].bytes == g.piece) {
-        cand.push_back(g_pieces[k]);
-        g_pieces.erase(g_pieces.begin() + k);
-      } else {
-        ++k;
-      }
-    }
-  }
-  hipStream_t s = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  struct Cleanup {
-    hipStream_t& s; hipEvent_t& a; hipEvent_t& b;
-    ~Cleanup() { if (a) (void)hipEventDestroy(a); if (b) (void)hipEventDestroy(b); if (s) (void)hipStreamDestroy(s); }
-  } cleanup{s, e0, e1};
-  if (g.pairing && (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) {
-    pool_put(cand);
-    return fail(FFMP_E_HIP, "ffmp_ring: stream/event creation failed");
-  }
-  int todo = 0;
-  for (char n : need) todo += n != 0;
-  const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
-  double ref = 0.0;                          // best probe seen: the scale "fast" is judged against
-  bool found_fast = false;
-  int fresh = 0;
-  hipError_t e = hipSuccess;
-  for (size_t pos = 0; pos < need.size(); ++pos) {
-    if (!need[pos]) continue;
-    const int j = (int)(pos % (size_t)g.per_slot);
-    const size_t off = (size_t)j * g.piece;
-    char* pb = g.pairing ? (char*)partner + off : nullptr;
-    const size_t pbytes = g.pairing && (int64_t)off < partner_bytes ? std::min(g.piece, (size_t)(partner_bytes - (int64_t)off)) : 0;
-    // no probe has found a fast pair in the first 12: the partner sits where nothing pairs
-    // well (seen at C5), so stop paying for probes and extra pieces
-    const bool test = g.pairing && pbytes >= (64u << 20) && (found_fast || r->pieces_tested < 12);
-    int pick = -1, here = 0;
-    double pick_gbs = -1.0;
-    size_t k = 0;
-    for (;;) {
-      int c = -1;
-      if (k < cand.size() && k < 6) {
-        c = (int)k++;
-      } else if (fresh < max_new && (fresh < todo || room_for(g.piece))) {
-        ffmp_piece p;
-        if ((e = new_piece(device, g.piece, g.gran, &p)) != hipSuccess) {
-          (void)hipGetLastError();
-          if (pick >= 0 || !cand.empty()) break;  // out of memory: settle for what there is
-          pool_put(cand);
-          return fail(FFMP_E_HIP, "ffmp_ring: hipMemCreate/map of a %zu-byte piece: %s", g.piece, hipGetErrorString(e));
-        }
-        ++fresh;
-        cand.push_back(p);
-        c = (int)cand.size() - 1;
-        k = cand.size();
-      } else {
-        break;
-      }
-      if (!test) {
-        pick = c;
-        break;
-      }
-      const double gbs = pair_gbs(cand[c].home, pb, pbytes, s, e0, e1);
-      ++r->pieces_tested;
-      ++here;
-      if (gbs >= kPairFastGBs) found_fast = true;
-      if (gbs > ref) ref = gbs;
-      if (gbs > pick_gbs) {
-        pick = c;
-        pick_gbs = gbs;
-      }
-      if (r->pieces_tested >= 3 && pick_gbs >= 0.93 * ref) break;
-      if (here >= 12) break;  // bounded search: keep the best seen
-    }
-    if (pick < 0) {
-      pool_put(cand);
-      return fail(FFMP_E_HIP, "ffmp_ring: no piece available");
-    }
-    if (test) {
-      r->pair_gbs_min = r->pair_gbs_min > 0 ? std::min(r->pair_gbs_min, pick_gbs) : pick_gbs;
-      r->pair_gbs_max = std::max(r->pair_gbs_max, pick_gbs);
-    }
-    r->pieces[pos] = cand[pick];
-    cand.erase(cand.begin() + pick);
-  }
-  r->pieces_new += fresh;
-  pool_put(cand);
-  pool_put(avoid);
-  return FFMP_OK;
-}
-
-// reserve the ring's own addresses and map slots 0..W-1, then slot 0's pieces again
-int ring_map(ffmp_ring* r, const RingGeom& g) {
-  // aligned to the piece (up to 1 GiB) so that every piece maps with the largest page fragments
-  hipError_t e = hipMemAddressReserve((void**)&r->va, r->vbytes, va_align(g.piece, g.gran), nullptr, 0);
-  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipMemAddressReserve: %s", hipGetErrorString(e));
-  for (int v = 0; v <= r->slots; ++v) {
-    const int slot = v % r->slots;
-    for (int j = 0; j < g.per_slot; ++j) {
-      const ffmp_piece& p = r->pieces[(size_t)slot * g.per_slot + j];
-      if ((e = map_rw(r->va + (size_t)v * r->stride + (size_t)j * g.piece, g.piece, p.h, r->device)) != hipSuccess)
-        return fail(FFMP_E_HIP, "ffmp_ring: hipMemMap: %s", hipGetErrorString(e));  // never reused
-    }
-  }
-  return FFMP_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const void* partner, int64_t partner_bytes,
-                     ffmp_ring_t** ring, void** base, int64_t* slot_stride) {
-  if (!ring || !base || !slot_stride) return fail(FFMP_E_ARG, "ffmp_ring_create: NULL output pointer");
-  *ring = nullptr;
-  *base = nullptr;
-  if (slot_bytes <= 0 || slots < 2) return fail(FFMP_E_ARG, "ffmp_ring_create: slot_bytes > 0 and slots >= 2 required");
-  if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_create: partner_bytes must be > 0");
-  DeviceScope scope(device);
-  RingGeom g;
-  if (const int rc = ring_geom(device, slot_bytes, partner, &g)) return rc;
-  std::unique_ptr<ffmp_ring> r(new ffmp_ring());
-  r->device = device;
-  r->slots = slots;
-  r->stride = g.stride;
-  r->vbytes = g.stride * (size_t)(slots + 1);
-  r->pieces.resize((size_t)slots * g.per_slot);
-  const std::vector<char> need(r->pieces.size(), 1);
-  if (const int rc = choose_pieces(r.get(), g, need, (const char*)partner, partner_bytes, {})) return rc;
-  if (const int rc = ring_map(r.get(), g)) {
-    pool_put(r->pieces);
-    return rc;
-  }
-  r->refs = 1;
-  *base = r->va;
-  *slot_stride = (int64_t)r->stride;
-  *ring = r.release();
-  return FFMP_OK;
-}
-
-int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partner, int64_t partner_bytes,
-                      ffmp_ring_t** ring, void** base, int64_t* slot_stride) {
-  if (!old || !ring || !base || !slot_stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: NULL argument");
-  *ring = nullptr;
-  *base = nullptr;
-  if (old->slots > 64) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: more than 64 slots");
-  if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: partner_bytes must be > 0");
-  DeviceScope scope(old->device);
-  RingGeom g;
-  if (const int rc = ring_geom(old->device, (int64_t)old->stride, partner, &g)) return rc;
-  if (g.stride != old->stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: geometry changed");
-  std::unique_ptr<ffmp_ring> r(new ffmp_ring());
-  r->device = old->device;
-  r->slots = old->slots;
-  r->stride = old->stride;
-  r->vbytes = old->vbytes;
-  r->pieces.resize(old->pieces.size());
-  std::vector<char> need(r->pieces.size(), 0);
-  std::vector<ffmp_piece> avoid, keep;
-  for (size_t pos = 0; pos < old->pieces.size(); ++pos) {
-    const int slot = (int)(pos / (size_t)g.per_slot);
-    if ((replace_mask >> slot) & 1u) {
-      need[pos] = 1;
-      avoid.push_back(old->pieces[pos]);
-    } else {
-      r->pieces[pos] = old->pieces[pos];
-    }
-  }
-  if (const int rc = choose_pieces(r.get(), g, need, (const char*)partner, partner_bytes, avoid)) return rc;
-  if (const int rc = ring_map(r.get(), g)) {
-    // the kept pieces still belong to `old`; give back only the new ones
-    std::vector<ffmp_piece> fresh;
-    for (size_t pos = 0; pos < need.size(); ++pos)
-      if (need[pos]) fresh.push_back(r->pieces[pos]);
-    pool_put(fresh);
-    return rc;
-  }
-  // ownership: `old` keeps nothing (its replaced pieces are pooled, its kept ones moved here);
-  // its addresses stay mapped and are never used again
-  old->pieces.clear();
-  r->pieces_new += old->pieces_new;
-  r->pieces_tested += old->pieces_tested;
-  r->refs = 1;
-  *base = r->va;
-  *slot_stride = (int64_t)r->stride;
-  *ring = r.release();
-  return FFMP_OK;
-}
-
-int ffmp_ring_destroy(ffmp_ring_t* ring) {
-  if (ring) ring_unref(ring);
-  return FFMP_OK;
-}
-
-int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap) {
-  if (!ring || !out || cap < 5) return fail(FFMP_E_ARG, "ffmp_ring_info: ring/out NULL or cap < 5");
-  out[0] = (double)ring->pieces.size();
-  out[1] = (double)ring->pieces_new;
-  out[2] = (double)ring->pieces_tested;
-  out[3] = ring->pair_gbs_min;
-  out[4] = ring->pair_gbs_max;
-  return 5;
-}
-
-int64_t ffmp_ring_pool_bytes(int32_t device) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  int64_t b = 0;
-  for (const ffmp_piece& p : g_pieces)
-    if (p.device == device || device < 0) b += (int64_t)p.bytes;
-  return b;
-}
-
-static void dl_delete(DLManagedTensor_* mt) {
-  DLHolder_* h = (DLHolder_*)mt->manager_ctx;
-  if (h->owner) ring_unref(h->owner);
-  free(h);
-}
-
-void* ffmp_dlpack(void* data, int32_t device_type, int32_t device_id, int32_t ndim, const int64_t* shape,
-                  const int64_t* strides, int32_t bits, ffmp_ring_t* owner) {
-  if (!data || ndim < 1 || ndim > 8 || !shape || !strides || (bits != 8 && bits != 16 && bits != 32 && bits != 64)) {
-    fail(FFMP_E_ARG, "ffmp_dlpack: bad arguments");
-    return nullptr;
-  }
-  DLHolder_* h = (DLHolder_*)calloc(1, sizeof(DLHolder_));
-  if (!h) {
-    fail(FFMP_E_ARG, "ffmp_dlpack: out of host memory");
-    return nullptr;
-  }
-  for (int d = 0; d < ndim; ++d) {
-    h->dims[d] = shape[d];
-    h->dims[8 + d] = strides[d];
-  }
-  h->mt.dl_tensor.data = data;
-  h->mt.dl_tensor.device = {device_type, device_id};
-  h->mt.dl_tensor.ndim = ndim;
-  h->mt.dl_tensor.dtype = {2 /* kDLFloat */, (uint8_t)bits, 1};
-  h->mt.dl_tensor.shape = h->dims;
-  h->mt.dl_tensor.strides = h->dims + 8;
-  h->mt.manager_ctx = h;
-  h->mt.deleter = dl_delete;
-  h->owner = owner;
-  if (owner) __atomic_add_fetch(&owner->refs, 1, __ATOMIC_ACQ_REL);
-  return &h->mt;
 }
 
 }  // extern "C"

@@ -54,6 +54,10 @@ def parse():
                    help="frame ring with frame_window > 2: seamless (VMM alias, never wraps) or wrap")
     p.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                    help="one-launch step (ffmp_step_fused) on/off, or auto: the instance's autotune decides")
+    p.add_argument("--save-tuning", default=None, help="write the instance's launch choices (JSON) here")
+    p.add_argument("--tuning", default=None,
+                   help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
+                        "launches of the dominant kernel in the trace)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -182,7 +186,11 @@ def main():
     n_total = n * world
     env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
                   frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring],
-                  fused={"auto": None, "on": True, "off": False}[args.fused])
+                  fused={"auto": None, "on": True, "off": False}[args.fused],
+                  tuning=json.load(open(args.tuning)) if args.tuning else None)
+    if args.save_tuning and rank == 0:
+        with open(args.save_tuning, "w") as f:
+            json.dump(env.tuning(), f)
 
     K, W = args.steps, args.warmup
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)

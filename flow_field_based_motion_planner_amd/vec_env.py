@@ -67,6 +67,9 @@ class FFMPVec:
         fused: True: every step is ONE launch (ffmp_step_fused: one block per env steps the env,
             then rasters its plane); False: the env kernel, then the raster; None (default): the
             autotune times both on this instance and keeps the faster (small batches: False).
+        tuning: a previous instance's `tuning()` (launch shapes, one- or two-launch step): used
+            instead of the autotune (e.g. for profiling runs that should contain only timed
+            launches); the seamless ring's slot repair still runs.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -74,7 +77,7 @@ class FFMPVec:
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
                  frame_window: Optional[int] = None, seamless: Optional[bool] = None,
-                 fused: Optional[bool] = None):
+                 fused: Optional[bool] = None, tuning: Optional[dict] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -122,11 +125,16 @@ class FFMPVec:
         self._build_structs()
         plane_bytes = self._nbytes((self.num_envs, (3 if potential else 2) + (2 if self.cfg.flow else 0), G2),
                                    torch.float32)
-        if autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
+        paired = self.ring == "seamless" and self.with_potential
+        if tuning is not None:
+            self._apply_tuning(tuning)
+            if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
+                self._repair_slots()
+                self.placement = dict(self.placement, ring=self.ring_meta)
+        elif autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
             self._autotune_raster()
             # the seamless ring already paired its slots with the potential plane; a new arena
             # would undo that
-            paired = self.ring == "seamless" and self.with_potential
             if self.arena and plane_bytes >= self.REPLACE_MIN_BYTES and not paired:
                 self._retry_placement()
             if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
@@ -388,6 +396,21 @@ class FFMPVec:
             self.potential.zero_()
             self._build_structs()
         self.ring_meta = dict(self._ring.info(), repair=history)
+
+    def tuning(self) -> dict:
+        """The launch choices of this instance (pass as FFMPVec(tuning=...) to skip the autotune)."""
+        return {"shape": list(self.raster_shape), "shape_newest": list(self.raster_shape_newest),
+                "fused": bool(self.fused), "fused_flags": int(self.fused_flags)}
+
+    def _apply_tuning(self, t: dict) -> None:
+        self.raster_shape = tuple(t["shape"])
+        self.raster_shape_newest = tuple(t.get("shape_newest", t["shape"]))
+        self.fused = bool(t.get("fused", False)) and self.pipeline_slices == 1 and self._fused_req is not False
+        self.fused_flags = int(t.get("fused_flags", _abi.RASTER_NT))
+        self.placement = {"shape": {"cells_per_block": self.raster_shape[0], "flags": self.raster_shape[1]},
+                          "shape_newest": {"cells_per_block": self.raster_shape_newest[0],
+                                           "flags": self.raster_shape_newest[1]},
+                          "from": "tuning", "fused": {"chosen": self.fused, "flags": self.fused_flags}}
 
     def _tune_steps(self) -> int:
         """Timed steps per measurement: >= ~10 ms of raster, in whole ring cycles — the wrapping

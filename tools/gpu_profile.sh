@@ -12,14 +12,16 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.build()" || exit 1
 # 49 timed steps = 7 whole frame-window cycles (W = 8), so trace and PMC passes average the same
 # mix of full and newest-only raster launches
-BENCH="$R/bench.py --config $CFG --steps 49 --warmup 10 --cpu-seconds 0"
+# the launch choices come from one plain run first, so that the profiled runs contain no
+# autotune launches: the trace's per-kernel average is then the timed launches' (plus warm-up)
+echo "== tuning run"
+timeout -k 10 300 python3 $R/bench.py --config $CFG --steps 8 --warmup 2 --cpu-seconds 0 --save-tuning $R/gpurun_out/prof/tuning_$CFG.json > $R/gpurun_out/prof/bench_tuning_$CFG.log 2>&1 || exit 1
+cat $R/gpurun_out/prof/tuning_$CFG.json; echo
+BENCH="$R/bench.py --config $CFG --steps 49 --warmup 10 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$CFG.json"
 echo "== trace"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/trace_$CFG -o run -- python3 $BENCH > $R/gpurun_out/prof/bench_trace_$CFG.log 2>&1 || exit 1
-# the PMC passes run the mode the trace run's autotune chose (one launch or two), so that their
-# per-launch bytes describe the same kernel
-FUSED=$(python3 -c "import json;d=json.loads([l for l in open('$R/gpurun_out/prof/bench_trace_$CFG.log') if l.startswith('{')][0]);print('on' if d['config'].get('fused') else 'off')")
-echo "== pmc write (fused=$FUSED)"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 --fused $FUSED > $R/gpurun_out/prof/bench_pmcw_$CFG.log 2>&1 || exit 1
+echo "== pmc write"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$CFG.json > $R/gpurun_out/prof/bench_pmcw_$CFG.log 2>&1 || exit 1
 echo "== pmc fetch"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 --fused $FUSED > $R/gpurun_out/prof/bench_pmcf_$CFG.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$CFG -o run -- python3 $R/bench.py --config $CFG --steps 49 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$CFG.json > $R/gpurun_out/prof/bench_pmcf_$CFG.log 2>&1 || exit 1
 cd $R && python3 tools/summarize_profiles.py $TAG $CFG

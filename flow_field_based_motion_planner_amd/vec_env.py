@@ -202,8 +202,10 @@ class FFMPVec:
         the device supports it; its slots are built to pair well with the potential plane the
         raster writes beside them (include/ffmp.h ffmp_ring_create)."""
         N, G = self.num_envs, self.cfg.grid
+        torch.cuda.synchronize(self.device)  # the pairing probes write the potential plane on their own stream
         try:
-            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, partner=self.potential)
+            partner = self.potential if self.PAIR_SLOTS else None
+            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, partner=partner)
             self.frames = self._ring.tensor
             self.ring_meta = self._ring.info()
         except _abi.FFMPBackendError:
@@ -366,6 +368,7 @@ class FFMPVec:
     # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.
     SLOW_SLOT = 1.06
     REPAIR_ROUNDS = 1
+    PAIR_SLOTS = True  # build the ring's slots from pieces probed against the potential plane
 
     def _slot_ms(self) -> Dict[int, float]:
         """Median newest-only raster ms per physical slot written, over two ring cycles."""
@@ -446,7 +449,7 @@ class FFMPVec:
         self.reset()  # a real state (a zeroed record would stack every disc on the robot cell)
         results = []
         steps = self._tune_steps()
-        for shape in self.RASTER_SHAPES:
+        for shape in self._shape_candidates():
             self.raster_shape = self.raster_shape_newest = shape
             results.append((self._raster_gbs_steady(steps), shape))
         best = {}
@@ -478,6 +481,14 @@ class FFMPVec:
         _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE2, _abi.RASTER_NT | _abi.RASTER_TILE8,
     )
 
+    XCD_SHAPES = True  # autotune candidates include the XCD-aware block remap
+
+    def _shape_candidates(self):
+        return [sh for sh in self.RASTER_SHAPES if self.XCD_SHAPES or not sh[1] & _abi.RASTER_XCD]
+
+    def _fused_candidates(self):
+        return [f for f in self.FUSED_FLAGS if self.XCD_SHAPES or not f & _abi.RASTER_XCD]
+
     def _tune_fused(self, steps: int) -> Optional[dict]:
         """Time whole steps of the two-launch path (the tuned raster shapes) against the fused
         step for each FUSED_FLAGS candidate; keep the faster (fused=None), or the best fused flags
@@ -489,7 +500,7 @@ class FFMPVec:
         sep = self._raster_gbs_steady(steps)["step_ms"]
         self.fused = True
         res = []
-        for f in self.FUSED_FLAGS:
+        for f in self._fused_candidates():
             self.fused_flags = f
             res.append((self._raster_gbs_steady(steps)["step_ms"], f))
         best_ms, best_f = min(res)

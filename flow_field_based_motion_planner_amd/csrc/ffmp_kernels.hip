@@ -428,9 +428,23 @@ FFMP_DEV int64_t logical_block() {
   return lb;
 }
 
+// A record word.  FRESH: the record was written earlier in this launch (by wave 0 of the block,
+// step_raster_kernel): load it device-coherently (bypassing the CU's vector L1, which may hold
+// a line shared with a neighbouring env's record read by another block on the CU).
+template <bool FRESH>
+FFMP_DEV float rec_word(const float* p) {
+  if (FRESH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+template <bool FRESH>
+FFMP_DEV float4 rec_word4(const float* p) {
+  return make_float4(rec_word<FRESH>(p), rec_word<FRESH>(p + 1), rec_word<FRESH>(p + 2), rec_word<FRESH>(p + 3));
+}
+
 // The raster of cells [tile * cells_per_block, ...) of env e by the whole 256-thread block
 // (block-uniform arguments; contains a block barrier).
-template <bool NT, bool FLOW>
+template <bool NT, bool FLOW, bool FRESH = false>
 FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, int64_t e, int tile, int32_t cells_per_block,
                                                         const float* __restrict__ record,
                                                         float* __restrict__ state_m, int64_t sm_stride,
@@ -443,13 +457,13 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   const int G2 = G * G;
   const int tid = threadIdx.x;
   const float* rec = record + e * rec_stride(K);
-  if (tid < FFMP_REC_HDR) s_hdr[tid] = rec[tid];
+  if (tid < FFMP_REC_HDR) s_hdr[tid] = rec_word<FRESH>(rec + tid);
   if (tid < K) {
-    const float4* ro = reinterpret_cast<const float4*>(rec + FFMP_REC_HDR);
-    s_cur[tid] = ro[tid];
-    s_prev[tid] = ro[K + tid];
+    const float* ro = rec + FFMP_REC_HDR;
+    s_cur[tid] = rec_word4<FRESH>(ro + 4 * tid);
+    s_prev[tid] = rec_word4<FRESH>(ro + 4 * (K + tid));
     if (FLOW) {
-      const float4 v = ro[2 * K + tid];
+      const float4 v = rec_word4<FRESH>(ro + 4 * (2 * K + tid));
       s_vel[tid] = make_float2(v.x, v.y);
     }
   }
@@ -623,9 +637,11 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   if (threadIdx.x < 64)
     env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
                                  s_ecur, s_eprev);
-  __threadfence_block();  // the record (global) is read by every wave below
+  // wave 0's record stores complete (write-through to the XCD's L2) before the barrier; the
+  // waves below read them L1-bypassing (an agent-scope fence here would write back the L2)
+  __threadfence_block();
   __syncthreads();
-  raster_env<NT, FLOW>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
+  raster_env<NT, FLOW, true>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
                        ob.potential, ob.flow, tile_log2r, s_cur, s_prev, s_vel, s_hdr);
 }
 

@@ -179,14 +179,6 @@ struct DeviceScope {
   }
 };
 
-}  // namespace
-
-extern "C" {
-
-}  // extern "C"
-
-namespace {
-
 struct RingGeom {
   size_t gran, piece, stride;
   int per_slot;

@@ -820,6 +820,7 @@ class FFMPVec:
         for name, _, _ in self._buffer_specs():
             setattr(self, name, None)
         self._arena_buf = None
+        self._ring = None  # the seamless ring's pieces return to the process pool
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ utilities

@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--tuning", default=None,
                    help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
                         "launches of the dominant kernel in the trace)")
+    p.add_argument("--obs-format", default="f32", choices=["f32", "u8f16"],
+                   help="f32: the reference consumer layout (state_m float32, the bench metric); u8f16: the "
+                        "compact layout (uint8 frames, float16 potential) for consumers that convert on load")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -131,16 +134,17 @@ def cpu_baseline_parallel(cfg, seconds: float, procs: int):
                       f"1 thread per process"}
 
 
-def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool):
+def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}{'' if obs_format == 'f32' else '_' + obs_format}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
         if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window \
-                or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused:
+                or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused \
+                or d.get("obs_format", "f32") != obs_format:
             return None
         return float(d["raster_hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
@@ -178,7 +182,8 @@ def main():
     n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
     # a strong-scaling preset (C4/C5) on fewer GPUs than it is quoted on may not fit one
     # GPU's HBM: then every rank runs the preset's per-GPU share instead (weak scaling)
-    per_env = 4 * cfg.grid * cfg.grid * (2 + (0 if args.no_potential else 1)) + 4096
+    fb, pb = (4, 4) if args.obs_format == "f32" else (1, 2)
+    per_env = cfg.grid * cfg.grid * (2 * fb + (0 if args.no_potential else pb)) + 4096
     budget = int(0.7 * torch.cuda.get_device_properties(dev).total_memory)
     if not args.envs and strong and n * per_env > budget:
         n = pr["n_envs"] // pr["gpus"]
@@ -187,7 +192,7 @@ def main():
     env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
                   frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring],
                   fused={"auto": None, "on": True, "off": False}[args.fused],
-                  tuning=json.load(open(args.tuning)) if args.tuning else None)
+                  tuning=json.load(open(args.tuning)) if args.tuning else None, obs_format=args.obs_format)
     if args.save_tuning and rank == 0:
         with open(args.save_tuning, "w") as f:
             json.dump(env.tuning(), f)
@@ -230,14 +235,14 @@ def main():
         print("raster ms per launch:", " ".join(f"{x:.3f}" for x in r_ms), file=sys.stderr, flush=True)
     n_full = sum(1 for r in raster_ev if r[4])
     G2 = cfg.grid * cfg.grid
-    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * 4 * G2
+    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * fb * G2
     raster_ms = sum(r_ms) / len(r_ms)
     step_ms_ev = sum(a.elapsed_time(b) for a, b in evs) / K
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
-                           seamless=env.ring == "seamless")
+                           seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
     per_launch_envs = raster_ev[0][2]
-    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring, env.fused)
+    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring, env.fused, args.obs_format)
 
     if rank == 0:
         out = {
@@ -251,11 +256,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.obs_format == "f32" else "u8 frames / f16 potential (f32 compute)",
             "data": "synthetic",
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
-                       "potential": not args.no_potential, "flow": bool(args.flow),
+                       "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
                        "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},

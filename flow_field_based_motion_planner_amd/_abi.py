@@ -16,7 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+OBS_F32, OBS_U8F16 = 0, 1  # include/ffmp.h FFMP_OBS_*
 
 
 class FFMPBackendError(RuntimeError):
@@ -49,7 +50,8 @@ class StateT(C.Structure):
 class ObsT(C.Structure):
     _fields_ = [("state_m", C.c_void_p), ("state_g", C.c_void_p), ("state_v", C.c_void_p),
                 ("state_t", C.c_void_p), ("potential", C.c_void_p), ("grad", C.c_void_p), ("lidar", C.c_void_p),
-                ("flow", C.c_void_p), ("state_m_stride", C.c_int64), ("state_m_frame_stride", C.c_int64)]
+                ("flow", C.c_void_p), ("state_m_stride", C.c_int64), ("state_m_frame_stride", C.c_int64),
+                ("format", C.c_int32), ("reserved", C.c_int32)]
 
 
 class OutT(C.Structure):
@@ -183,6 +185,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
         0: C.sizeof(CfgT), 1: C.sizeof(StateT), 2: C.sizeof(ObsT), 3: C.sizeof(OutT),
         4: CfgT.res.offset, 5: CfgT.res_f.offset, 6: CfgT.seed.offset, 7: CfgT.beam_cs.offset,
         8: C.sizeof(EpisodeT),
+        9: ObsT.format.offset,
     }
     for k, v in want.items():
         got = lib.ffmp_layout(k)
@@ -193,6 +196,8 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
 TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES, TUNE_ENV_LANES = 1, 2, 3, 4, 5
 RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
 RASTER_TILE2, RASTER_TILE4, RASTER_TILE8 = 16, 32, 64
+RASTER_NARROW = 128  # FFMP_OBS_U8F16: 4 cells per lane instead of 16
+RASTER_TILE16 = 256
 
 
 def set_tuning(key: int, value: int) -> int:

@@ -196,6 +196,26 @@ FFMP_DEV float add_repulsive(const ffmp_cfg_t& cfg, float U, float ex, float ey,
   return U;
 }
 
+// add_repulsive for a cell whose squared distance s = dx*dx + dy*dy to the disc centre is already
+// computed (the same float32 operations, so the result is bit-identical), skipping the sqrt and
+// the division when s >= reach2 = rep_reach2(cfg, r): there sqrtf(s) - r >= rho0 for certain, so
+// the term is exactly zero.
+FFMP_DEV float rep_reach2(const ffmp_cfg_t& cfg, float r) {
+  const float a = cfg.rho0_f + r;
+  return (a * a) * 1.000004f;  // > ((rho0 + r)(1 + 2^-20))^2 despite the rounding of a, a*a and the product
+}
+
+FFMP_DEV float add_repulsive_s(const ffmp_cfg_t& cfg, float U, float s, float r, float reach2) {
+  if (s >= reach2) return U;
+  float d = sqrtf(s) - r;
+  d = fmaxf(d, cfg.rho_min_f);
+  if (d < cfg.rho0_f) {
+    const float q = 1.0f / d - cfg.inv_rho0_f;
+    U = U + cfg.half_kr_f * (q * q);
+  }
+  return U;
+}
+
 FFMP_DEV float attractive(const ffmp_cfg_t& cfg, float ex, float ey, float gx, float gy) {
   const float dx = ex - gx, dy = ey - gy;
   return cfg.half_ka_f * (dx * dx + dy * dy);

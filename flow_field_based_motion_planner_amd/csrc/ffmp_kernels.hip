@@ -14,6 +14,7 @@
 //   reward_done_kernel / footprint_kernel / scan_kernel — legacy FFMP methods.
 // The seamless frame ring (HIP virtual memory) and the DLPack hand-off: ffmp_ring.hip.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -69,6 +70,13 @@ int check_cfg(const ffmp_cfg_t* c) {
     if (i < 0 || j < 0 || i >= c->grid || j >= c->grid)
       return fail(FFMP_E_CFG, "footprint cell outside the grid (index %d)", f);
   }
+  return FFMP_OK;
+}
+
+int check_format(const ffmp_obs_t* o, bool flow) {
+  if (o->format != FFMP_OBS_F32 && o->format != FFMP_OBS_U8F16)
+    return fail(FFMP_E_ARG, "unknown obs.format %d", o->format);
+  if (o->format == FFMP_OBS_U8F16 && flow) return fail(FFMP_E_ARG, "obs.format U8F16 has no flow planes (cfg.flow)");
   return FFMP_OK;
 }
 
@@ -396,6 +404,51 @@ FFMP_DEV void store4(float* p, float a, float b, float c, float d) {
   else *reinterpret_cast<f32x4*>(p) = v;
 }
 
+// Compact observation format (FFMP_OBS_U8F16): a lane's 4 occupancy cells as 4 bytes (0 / 255)
+// in one dword store, its 4 potential cells as binary16 (round to nearest even, as numpy's
+// float32 -> float16 cast) in one dwordx2 store.
+FFMP_DEV uint32_t pack4_u8(const float occ[4]);
+
+template <bool NT>
+FFMP_DEV void store4_u8(uint8_t* p, const float occ[4]) {
+  const uint32_t v = pack4_u8(occ);
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(p));
+  else *reinterpret_cast<uint32_t*>(p) = v;
+}
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+FFMP_DEV uint32_t pack4_u8(const float occ[4]) {
+  return (occ[0] != 0.0f ? 0xFFu : 0u) | (occ[1] != 0.0f ? 0xFF00u : 0u) | (occ[2] != 0.0f ? 0xFF0000u : 0u) |
+         (occ[3] != 0.0f ? 0xFF000000u : 0u);
+}
+
+// 16 cells of a lane as one 16-B store (the frame) and two 16-B stores (the potential): whole
+// 16-B lane segments, as the float32 layout's, so nontemporal stores stay full-width
+template <bool NT>
+FFMP_DEV void store16_u8(uint8_t* p, const float occ[16]) {
+  u32x4 v = {pack4_u8(occ), pack4_u8(occ + 4), pack4_u8(occ + 8), pack4_u8(occ + 12)};
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = v;
+}
+
+template <bool NT>
+FFMP_DEV void store8_h(_Float16* p, const float* U) {
+  f16x8 v = {(_Float16)U[0], (_Float16)U[1], (_Float16)U[2], (_Float16)U[3],
+             (_Float16)U[4], (_Float16)U[5], (_Float16)U[6], (_Float16)U[7]};
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<f16x8*>(p));
+  else *reinterpret_cast<f16x8*>(p) = v;
+}
+
+template <bool NT>
+FFMP_DEV void store4_h(_Float16* p, float a, float b, float c, float d) {
+  f16x4 v = {(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<f16x4*>(p));
+  else *reinterpret_cast<f16x4*>(p) = v;
+}
+
 FFMP_DEV float box_dist2(float px, float py, float x0, float x1, float y0, float y1) {
   const float dx = fmaxf(fmaxf(x0 - px, px - x1), 0.0f);
   const float dy = fmaxf(fmaxf(y0 - py, py - y1), 0.0f);
@@ -409,7 +462,7 @@ FFMP_DEV bool corner_inside(const ffmp_cfg_t& cfg, const FrameHdr& h, float ex, 
   return (fabsf(wx) <= W) && (fabsf(wy) <= W);
 }
 
-// r / G for 0 <= r < 256 + G (8 <= G <= 4096): (r + 0.5) / G is >= 0.5/G away
+// r / G for 0 <= r < 1024 + G (8 <= G <= 4096): (r + 0.5) / G is >= 0.5/G away
 // from an integer, far more than the float32 error of the product.
 FFMP_DEV int small_div(int r, float invG) { return (int)(((float)r + 0.5f) * invG); }
 
@@ -442,9 +495,16 @@ FFMP_DEV float4 rec_word4(const float* p) {
   return make_float4(rec_word<FRESH>(p), rec_word<FRESH>(p + 1), rec_word<FRESH>(p + 2), rec_word<FRESH>(p + 3));
 }
 
+// Observation format of a raster instantiation: FMT_F32 (reference layout), FMT_CT4 (compact
+// FFMP_OBS_U8F16, 4 cells per lane) or FMT_CT16 (compact, 16 cells per lane: a wave task is
+// 1024 cells, so the per-task cull / wall / index work is spread over 4x the cells — the compact
+// raster writes 3 bytes per cell and is bound by that per-task work, not by HBM; needs G % 16 == 0).
+constexpr int FMT_F32 = 0, FMT_CT4 = 1, FMT_CT16 = 2;
+
 // The raster of cells [tile * cells_per_block, ...) of env e by the whole 256-thread block
-// (block-uniform arguments; contains a block barrier).
-template <bool NT, bool FLOW, bool FRESH = false>
+// (block-uniform arguments; contains a block barrier).  Compact formats: state_m holds uint8
+// frames and pot binary16 planes (the pointers are reinterpreted; strides in elements).
+template <bool NT, bool FLOW, int FMT, bool FRESH = false>
 FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, int64_t e, int tile, int32_t cells_per_block,
                                                         const float* __restrict__ record,
                                                         float* __restrict__ state_m, int64_t sm_stride,
@@ -452,6 +512,9 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
                                                         float* __restrict__ pot, float* __restrict__ flow,
                                                         int32_t tile_log2r, float4* s_cur, float4* s_prev,
                                                         float2* s_vel, float* s_hdr) {
+  constexpr bool CT = FMT != FMT_F32;
+  constexpr int CPL = FMT == FMT_CT16 ? 16 : 4;  // cells per lane in a wave task
+  constexpr int WC = 64 * CPL;                   // cells per wave task
   const int K = cfg.n_obst;
   const int G = cfg.grid;
   const int G2 = G * G;
@@ -494,13 +557,16 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   float* m0 = state_m + e * sm_stride;
   float* m1 = m0 + sm_frame;
   float* pp = pot ? pot + (int64_t)e * G2 : nullptr;
+  uint8_t* b0 = CT ? reinterpret_cast<uint8_t*>(state_m) + e * sm_stride : nullptr;
+  uint8_t* b1 = CT ? b0 + sm_frame : nullptr;
+  _Float16* hp16 = (CT && pot) ? reinterpret_cast<_Float16*>(pot) + (int64_t)e * G2 : nullptr;
   float* f0 = FLOW ? flow + (int64_t)e * 2 * G2 : nullptr;
 
   const int qbeg = tile * cells_per_block;
   const int qend = min(qbeg + cells_per_block, G2);
 
   // One wave task: the cells of ego rows [i0, i1] x columns [j0, j1] (the cull box), this
-  // lane's 4 cells (i, j..j+3) at plane offset q, `valid` = the lane has cells.
+  // lane's CPL cells (i, j..j+CPL-1) at plane offset q, `valid` = the lane has cells.
   auto task = [&](int i0, int i1, int j0, int j1, int i, int j, int q, bool valid) {
     const float bx0 = (float)i0 * res - half, bx1 = (float)i1 * res - half;
     const float by0 = (float)j0 * res - half, by1 = (float)j1 * res - half;
@@ -514,15 +580,15 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
     const bool walls_p = write_old && (wb & 0xF0ull) != 0xF0ull;
     if (!valid) return;
 
-    // ---- this lane's 4 cells ----
+    // ---- this lane's CPL cells ----
     const float ex = (float)i * res - half;
-    float ey[4];
+    float ey[CPL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ey[u] = (float)(j + u) * res - half;
+    for (int u = 0; u < CPL; ++u) ey[u] = (float)(j + u) * res - half;
 
-    float occp[4], occc[4], U[4];
+    float occp[CPL], occc[CPL], U[CPL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < CPL; ++u) {
       occp[u] = (walls_p && outside_world(cfg, hp, ex, ey[u])) ? 1.0f : 0.0f;
       occc[u] = (walls_c && outside_world(cfg, hc, ex, ey[u])) ? 1.0f : 0.0f;
       U[u] = with_pot ? attractive(cfg, ex, ey[u], gx, gy) : 0.0f;
@@ -530,24 +596,48 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
     for (uint64_t m = mp; m; m &= m - 1) {
       const float4 o = s_prev[__builtin_ctzll(m)];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) if (in_disc(ex, ey[u], o)) occp[u] = 1.0f;
+      for (int u = 0; u < CPL; ++u) if (in_disc(ex, ey[u], o)) occp[u] = 1.0f;
     }
-    float fx[4] = {0.f, 0.f, 0.f, 0.f}, fy[4] = {0.f, 0.f, 0.f, 0.f};
-    bool fset[4] = {false, false, false, false};
+    float fx[CPL], fy[CPL];
+    bool fset[CPL];
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+      fx[u] = fy[u] = 0.0f;
+      fset[u] = false;
+    }
     for (uint64_t m = mc; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
       const float4 o = s_cur[k];
+      const float reach2 = rep_reach2(cfg, o.w);
+      const float dx = ex - o.x;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool d = in_disc(ex, ey[u], o);
+      for (int u = 0; u < CPL; ++u) {
+        const float dy = ey[u] - o.y;
+        const float d2 = dx * dx + dy * dy;  // in_disc's and add_repulsive's operand
+        const bool d = d2 <= o.z;
         if (d) occc[u] = 1.0f;
         if (FLOW && d && !fset[u]) {  // lowest disc index covering the cell
           fx[u] = s_vel[k].x;
           fy[u] = s_vel[k].y;
           fset[u] = true;
         }
-        if (with_pot) U[u] = add_repulsive(cfg, U[u], ex, ey[u], o);
+        if (with_pot) U[u] = add_repulsive_s(cfg, U[u], d2, o.w, reach2);
       }
+    }
+    if (CT && CPL == 16) {
+      if (write_old) store16_u8<NT>(b0 + q, occp);
+      store16_u8<NT>(b1 + q, occc);
+      if (hp16) {
+        store8_h<NT>(hp16 + q, U);
+        store8_h<NT>(hp16 + q + 8, U + 8);
+      }
+      return;
+    }
+    if (CT) {
+      if (write_old) store4_u8<NT>(b0 + q, occp);
+      store4_u8<NT>(b1 + q, occc);
+      if (hp16) store4_h<NT>(hp16 + q, U[0], U[1], U[2], U[3]);
+      return;
     }
     if (write_old) store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
     store4<NT>(m1 + q, occc[0] * 255.0f, occc[1] * 255.0f, occc[2] * 255.0f, occc[3] * 255.0f);
@@ -559,43 +649,43 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   };
 
   if (tile_log2r > 0) {
-    // 2-D wave tiles of R rows x C = 256/R columns (the host checked G % C == 0 and that the
+    // 2-D wave tiles of R rows x C = WC/R columns (the host checked G % C == 0 and that the
     // block holds whole bands of R rows): a compact cull box (C3, R = 4: 0.2 m x 3.2 m instead
-    // of one 12.8 m row), so far fewer discs survive the cull; every row segment is C*4 bytes
-    // of contiguous, 16-B-per-lane stores.  Tiles are dealt band-major to the 4 waves, so the
-    // waves of a block write neighbouring columns of the same rows at once.
-    const int R = 1 << tile_log2r, C = 256 >> tile_log2r;
+    // of one 12.8 m row), so far fewer discs survive the cull; every row segment is C cells
+    // of contiguous, 4*CPL-byte-per-lane (float32) stores.  Tiles are dealt band-major to the 4
+    // waves, so the waves of a block write neighbouring columns of the same rows at once.
+    const int R = 1 << tile_log2r, C = WC >> tile_log2r;
     const int lanes_per_row = 64 >> tile_log2r;
     const int ncb = G / C;
     const int row0 = qbeg / G;
     const int ntiles = ((qend - qbeg) / G / R) * ncb;
     const int r = lane / lanes_per_row;
-    const int c4 = (lane - r * lanes_per_row) * 4;
+    const int cl = (lane - r * lanes_per_row) * CPL;
     for (int t = wave; t < ntiles; t += 4) {
       const int band = t / ncb;
       const int cb = t - band * ncb;
       const int i0 = row0 + band * R, j0 = cb * C;
-      const int i = i0 + r, j = j0 + c4;
+      const int i = i0 + r, j = j0 + cl;
       task(i0, i0 + R - 1, j0, j0 + C - 1, i, j, i * G + j, true);
     }
   } else {
-    for (int q0 = qbeg + wave * 256; q0 < qend; q0 += 1024) {
-      // ---- wave chunk [q0, qlast] (256 consecutive cells) -> ego bounding box ----
-      const int qlast = min(q0 + 255, G2 - 1);
+    for (int q0 = qbeg + wave * WC; q0 < qend; q0 += 4 * WC) {
+      // ---- wave chunk [q0, qlast] (WC consecutive cells) -> ego bounding box ----
+      const int qlast = min(q0 + WC - 1, G2 - 1);
       const int i0 = q0 / G;
       const int r0 = q0 - i0 * G;
       const int i1 = i0 + small_div(r0 + (qlast - q0), invG);
       int j0 = 0, j1 = G - 1;
       if (i0 == i1) { j0 = r0; j1 = r0 + (qlast - q0); }
-      const int off = r0 + lane * 4;
-      const int q = q0 + lane * 4;
+      const int off = r0 + lane * CPL;
+      const int q = q0 + lane * CPL;
       const int di = small_div(off, invG);
       task(i0, i1, j0, j1, i0 + di, off - di * G, q, q < qend);
     }
   }
 }
 
-template <bool NT, bool XCD, bool FLOW>
+template <bool NT, bool XCD, bool FLOW, int FMT>
 __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
@@ -612,7 +702,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   const int tile = (int)(lb - e * bpe);
   if (e >= n) return;
   if (mask && !mask[e]) return;
-  raster_env<NT, FLOW>(cfg, e, tile, cells_per_block, record, state_m, sm_stride, sm_frame, newest_only, pot, flow,
+  raster_env<NT, FLOW, FMT>(cfg, e, tile, cells_per_block, record, state_m, sm_stride, sm_frame, newest_only, pot, flow,
                        tile_log2r, s_cur, s_prev, s_vel, s_hdr);
 }
 
@@ -621,7 +711,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
 // env's whole plane from the record it just wrote.  The env step's float64 work of one block
 // overlaps the store streams of the other blocks on the CU, instead of running as its own
 // launch before the raster (~4 % of a C3 step).
-template <bool NT, bool XCD, bool FLOW>
+template <bool NT, bool XCD, bool FLOW, int FMT>
 __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                           const int64_t* __restrict__ action, ffmp_state_t st,
                                                           ffmp_obs_t ob, ffmp_out_t out, int64_t sm_stride,
@@ -641,7 +731,7 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   // waves below read them L1-bypassing (an agent-scope fence here would write back the L2)
   __threadfence_block();
   __syncthreads();
-  raster_env<NT, FLOW, true>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
+  raster_env<NT, FLOW, FMT, true>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
                        ob.potential, ob.flow, tile_log2r, s_cur, s_prev, s_vel, s_hdr);
 }
 
@@ -847,6 +937,44 @@ void launch_env_lpe(int mode, int lpe, const ffmp_cfg_t& cfg, int64_t n, int64_t
 // ============================================================================
 // C ABI
 // ============================================================================
+namespace {
+
+// log2 of the rows of a 2-D wave tile (FFMP_RASTER_TILE*), 0 = 1-D chunks
+int32_t tile_rows_log2(int32_t flags) {
+  return (flags & FFMP_RASTER_TILE16) ? 4 : (flags & FFMP_RASTER_TILE8) ? 3 : (flags & FFMP_RASTER_TILE4) ? 2
+       : (flags & FFMP_RASTER_TILE2) ? 1 : 0;
+}
+
+// The raster instantiation for an obs format: compact planes use 16 cells per lane when every
+// lane's 16 cells stay in one row (G % 16 == 0) unless FFMP_RASTER_NARROW asks for 4.
+int raster_format(bool compact, int grid, int32_t flags) {
+  if (!compact) return FMT_F32;
+  return (grid % 16 == 0 && !(flags & FFMP_RASTER_NARROW)) ? FMT_CT16 : FMT_CT4;
+}
+
+// Calls f(NT, XCD, FLOW, FMT) with std::integral_constant arguments for the runtime choice (the
+// compact formats have no flow planes: check_format refused them before).
+template <class F>
+void dispatch_variant(int fmt, bool nt, bool xcd, bool fl, F&& f) {
+  using T = std::true_type;
+  using N = std::false_type;
+  auto with_fmt = [&](auto NT_, auto XCD_) {
+    if (fmt == FMT_CT16) f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT16>{});
+    else if (fmt == FMT_CT4) f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT4>{});
+    else if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_F32>{});
+    else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_F32>{});
+  };
+  if (nt) {
+    if (xcd) with_fmt(T{}, T{});
+    else with_fmt(T{}, N{});
+  } else {
+    if (xcd) with_fmt(N{}, T{});
+    else with_fmt(N{}, N{});
+  }
+}
+
+}  // namespace
+
 extern "C" {
 
 int ffmp_abi_version(void) { return FFMP_ABI_VERSION; }
@@ -897,6 +1025,7 @@ int64_t ffmp_layout(int32_t which) {
     case 6: return (int64_t)offsetof(ffmp_cfg_t, seed);
     case 7: return (int64_t)offsetof(ffmp_cfg_t, beam_cs);
     case 8: return (int64_t)sizeof(ffmp_episode_t);
+    case 9: return (int64_t)offsetof(ffmp_obs_t, format);
     default: return -1;
   }
 }
@@ -944,7 +1073,7 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
       return fail(FFMP_E_ARG, "an out pointer is NULL");
   }
   if (n == 0) return FFMP_OK;
-  if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
+  if (n > 0x7fffffffLL / 64) return fail(FFMP_E_ARG, "n too large for one launch: %lld", (long long)n);  // <= 64 lanes per env
   ffmp_out_t o = out ? *out : ffmp_out_t{};
   const Tuning& tu = tuning();
   // lanes per env: at least K (lane k holds disc k); with many beams more lanes keep the lidar
@@ -979,48 +1108,54 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   if (cells_per_block != 0 && (cells_per_block < 1024 || cells_per_block % 1024 != 0))
     return fail(FFMP_E_ARG, "cells_per_block must be 0 or a multiple of 1024, got %d", cells_per_block);
   if ((flags & FFMP_RASTER_NT) && (flags & FFMP_RASTER_PLAIN)) return fail(FFMP_E_ARG, "NT and PLAIN both set");
+  if (int rc2 = check_format(obs, cfg->flow != 0)) return rc2;
   if (n == 0) return FFMP_OK;
   const int G2 = cfg->grid * cfg->grid;
   const int cpb_max = cells_per_block ? cells_per_block : 4096;
   const int cpb = G2 < cpb_max ? ((G2 + 1023) / 1024) * 1024 : cpb_max;
   const int bpe = (G2 + cpb - 1) / cpb;
-  const int64_t blocks = n * bpe;
-  if (blocks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many raster blocks: %lld", (long long)blocks);
+  // a launch holds at most 2^31 - 1 work-items: larger batches go out as several launches over
+  // consecutive env ranges (the whole C5 workload in the compact format is 131,072 x 64 blocks)
+  const int64_t max_envs = (0x7fffffffLL / 256) / bpe;
+  if (max_envs < 1) return fail(FFMP_E_ARG, "a raster plane needs too many blocks: %d", bpe);
   const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
   const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
   const bool fl = cfg->flow != 0;
   if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
+  const bool ct = obs->format == FFMP_OBS_U8F16;
   const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
   const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
   if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
-    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld floats (G*G = %d)",
+    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld elements (G*G = %d)",
                 (long long)sm_stride, (long long)sm_frame, G2);
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
   // 2-D wave tiles: R rows x 256/R columns, where the plane and the block split into them
-  int32_t tile_log2r = (flags & FFMP_RASTER_TILE8) ? 3 : (flags & FFMP_RASTER_TILE4) ? 2 : (flags & FFMP_RASTER_TILE2) ? 1 : 0;
+  const int fmt = raster_format(ct, cfg->grid, flags);
+  // 2-D wave tiles: R rows x (cells per wave task)/R columns, where the plane and the block split into them
+  int32_t tile_log2r = tile_rows_log2(flags);
   if (tile_log2r) {
-    const int C = 256 >> tile_log2r, R = 1 << tile_log2r;
+    const int C = (fmt == FMT_CT16 ? 1024 : 256) >> tile_log2r, R = 1 << tile_log2r;
     const bool whole_bands = cpb >= G2 || (cpb % (cfg->grid * R)) == 0;
     if ((cfg->grid % C) != 0 || !whole_bands) tile_log2r = 0;  // the 1-D chunks (identical results)
   }
-  const dim3 grid((unsigned)blocks), block(256);
+  const dim3 block(256);
   hipStream_t s = (hipStream_t)stream;
-#define FFMP_RASTER_LAUNCH(NT_, XCD_, FL_)                                                              \
-  hipLaunchKernelGGL((raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, bpe, cpb, record, mask, \
-                     obs->state_m, sm_stride, sm_frame, newest, obs->potential, obs->flow, tile_log2r)
-  const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
-  switch (sel) {
-    case 0: FFMP_RASTER_LAUNCH(false, false, false); break;
-    case 1: FFMP_RASTER_LAUNCH(false, false, true); break;
-    case 2: FFMP_RASTER_LAUNCH(false, true, false); break;
-    case 3: FFMP_RASTER_LAUNCH(false, true, true); break;
-    case 4: FFMP_RASTER_LAUNCH(true, false, false); break;
-    case 5: FFMP_RASTER_LAUNCH(true, false, true); break;
-    case 6: FFMP_RASTER_LAUNCH(true, true, false); break;
-    default: FFMP_RASTER_LAUNCH(true, true, true); break;
+  const int64_t rs = rec_stride(cfg->n_obst);
+  for (int64_t e0 = 0; e0 < n; e0 += max_envs) {
+    const int64_t m = n - e0 < max_envs ? n - e0 : max_envs;
+    const dim3 grid((unsigned)(m * bpe));
+    const float* rec = record + e0 * rs;
+    const uint8_t* msk = mask ? mask + e0 : nullptr;
+    float* sm = (float*)((char*)obs->state_m + e0 * sm_stride * (ct ? 1 : 4));
+    float* pot = obs->potential ? (float*)((char*)obs->potential + e0 * (int64_t)G2 * (ct ? 2 : 4)) : nullptr;
+    float* flw = obs->flow ? obs->flow + e0 * 2 * (int64_t)G2 : nullptr;
+    dispatch_variant(fmt, nt, xcd, fl, [&](auto NT_, auto XCD_, auto FL_, auto FMT_) {
+      hipLaunchKernelGGL((raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, 0, s, *cfg, m,
+                         bpe, cpb, rec, msk, sm, sm_stride, sm_frame, newest, pot, flw, tile_log2r);
+    });
+    if (int rc2 = check_launch("ffmp_raster")) return rc2;
   }
-#undef FFMP_RASTER_LAUNCH
-  return check_launch("ffmp_raster");
+  return FFMP_OK;
 }
 
 int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record, const uint8_t* mask, ffmp_obs_t* obs,
@@ -1055,37 +1190,30 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
   if ((flags & FFMP_RASTER_NT) && (flags & FFMP_RASTER_PLAIN)) return fail(FFMP_E_ARG, "NT and PLAIN both set");
   const bool fl = cfg->flow != 0;
   if (fl && !obs->flow) return fail(FFMP_E_ARG, "cfg.flow is set but obs.flow is NULL");
+  if (int rc2 = check_format(obs, fl)) return rc2;
+  const bool ct = obs->format == FFMP_OBS_U8F16;
   if (n == 0) return FFMP_OK;
-  if (n > 0x7fffffffLL) return fail(FFMP_E_ARG, "n too large: %lld", (long long)n);
+  if (n > 0x7fffffffLL / 256) return fail(FFMP_E_ARG, "n too large for one launch: %lld", (long long)n);  // one block per env
   const int G2 = cfg->grid * cfg->grid;
   const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
   const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
   if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
-    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld floats (G*G = %d)", (long long)sm_stride,
+    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld elements (G*G = %d)", (long long)sm_stride,
                 (long long)sm_frame, G2);
   const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
   const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
-  int32_t tile_log2r = (flags & FFMP_RASTER_TILE8) ? 3 : (flags & FFMP_RASTER_TILE4) ? 2 : (flags & FFMP_RASTER_TILE2) ? 1 : 0;
-  if (tile_log2r && (cfg->grid % (256 >> tile_log2r)) != 0) tile_log2r = 0;  // a block is one whole plane
+  const int fmt = raster_format(ct, cfg->grid, flags);
+  int32_t tile_log2r = tile_rows_log2(flags);
+  if (tile_log2r && (cfg->grid % ((fmt == FMT_CT16 ? 1024 : 256) >> tile_log2r)) != 0)
+    tile_log2r = 0;  // a block is one whole plane
   const dim3 grid((unsigned)n), block(256);
   hipStream_t s = (hipStream_t)stream;
   ffmp_out_t o = *out;
-#define FFMP_FUSED_LAUNCH(NT_, XCD_, FL_)                                                                     \
-  hipLaunchKernelGGL((step_raster_kernel<NT_, XCD_, FL_>), grid, block, 0, s, *cfg, n, env_offset, action, *state, \
-                     *obs, o, sm_stride, sm_frame, newest, tile_log2r)
-  const int sel = (nt ? 4 : 0) | (xcd ? 2 : 0) | (fl ? 1 : 0);
-  switch (sel) {
-    case 0: FFMP_FUSED_LAUNCH(false, false, false); break;
-    case 1: FFMP_FUSED_LAUNCH(false, false, true); break;
-    case 2: FFMP_FUSED_LAUNCH(false, true, false); break;
-    case 3: FFMP_FUSED_LAUNCH(false, true, true); break;
-    case 4: FFMP_FUSED_LAUNCH(true, false, false); break;
-    case 5: FFMP_FUSED_LAUNCH(true, false, true); break;
-    case 6: FFMP_FUSED_LAUNCH(true, true, false); break;
-    default: FFMP_FUSED_LAUNCH(true, true, true); break;
-  }
-#undef FFMP_FUSED_LAUNCH
+  dispatch_variant(fmt, nt, xcd, fl, [&](auto NT_, auto XCD_, auto FL_, auto FMT_) {
+    hipLaunchKernelGGL((step_raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, 0, s, *cfg, n,
+                       env_offset, action, *state, *obs, o, sm_stride, sm_frame, newest, tile_log2r);
+  });
   return check_launch("ffmp_step_fused");
 }
 

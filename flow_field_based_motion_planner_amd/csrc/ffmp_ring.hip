@@ -466,7 +466,8 @@ void* ffmp_dlpack(void* data, int32_t device_type, int32_t device_id, int32_t nd
   h->mt.dl_tensor.data = data;
   h->mt.dl_tensor.device = {device_type, device_id};
   h->mt.dl_tensor.ndim = ndim;
-  h->mt.dl_tensor.dtype = {2 /* kDLFloat */, (uint8_t)bits, 1};
+  // 8-bit elements are uint8 (the compact frames, FFMP_OBS_U8F16); wider ones are floats
+  h->mt.dl_tensor.dtype = {(uint8_t)(bits == 8 ? 1 /* kDLUInt */ : 2 /* kDLFloat */), (uint8_t)bits, 1};
   h->mt.dl_tensor.shape = h->dims;
   h->mt.dl_tensor.strides = h->dims + 8;
   h->mt.manager_ctx = h;

@@ -56,6 +56,8 @@ class Brain:
     @staticmethod
     def _q(net: Network, coupling: str, sm, sg, sv, st):
         prev, net.coupling = net.coupling, coupling
+        if sm.dtype == torch.uint8:  # FFMPVec(obs_format="u8f16"): the same 0/255 values, as float
+            sm = sm.float()
         try:
             return net(sm, sg, sv, st)
         finally:

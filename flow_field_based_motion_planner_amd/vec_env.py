@@ -70,6 +70,12 @@ class FFMPVec:
         tuning: a previous instance's `tuning()` (launch shapes, one- or two-launch step): used
             instead of the autotune (e.g. for profiling runs that should contain only timed
             launches); the seamless ring's slot repair still runs.
+        obs_format: "f32" (default): the reference consumer layout, state_m float32 0/255
+            (train.py:543-545) and a float32 potential plane.  "u8f16": the compact layout
+            (include/ffmp.h FFMP_OBS_U8F16) for consumers that convert on load — state_m uint8
+            with the same 0/255 values (`state_m.float()` is the f32 layout bit for bit) and the
+            potential plane as float16 (the float32 value rounded to nearest even): 3 instead of
+            8 bytes per cell of a step's raster.  No flow planes.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -77,7 +83,7 @@ class FFMPVec:
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
                  frame_window: Optional[int] = None, seamless: Optional[bool] = None,
-                 fused: Optional[bool] = None, tuning: Optional[dict] = None):
+                 fused: Optional[bool] = None, tuning: Optional[dict] = None, obs_format: str = "f32"):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -94,6 +100,14 @@ class FFMPVec:
         self.num_envs = int(num_envs)
         if self.num_envs <= 0:
             raise ValueError("num_envs must be positive")
+        if obs_format not in self.OBS_FORMATS:
+            raise ValueError(f"obs_format must be one of {sorted(self.OBS_FORMATS)}, got {obs_format!r}")
+        if obs_format == "u8f16" and config.flow:
+            raise ValueError('obs_format="u8f16" has no flow planes (config.flow)')
+        self.obs_format = obs_format
+        self._fmt, self._frame_dtype, self._pot_dtype = self.OBS_FORMATS[obs_format]
+        self._fes = torch.empty((), dtype=self._frame_dtype).element_size()  # bytes per frame cell
+        self._pes = torch.empty((), dtype=self._pot_dtype).element_size()    # bytes per potential cell
         self.env_offset = int(env_offset)
         self.with_potential = bool(potential)
         self.arena = bool(arena)
@@ -123,8 +137,8 @@ class FFMPVec:
         if self.pipeline_slices > 1:
             self._fused_req = False
         self._build_structs()
-        plane_bytes = self._nbytes((self.num_envs, (3 if potential else 2) + (2 if self.cfg.flow else 0), G2),
-                                   torch.float32)
+        plane_bytes = self.num_envs * G2 * (2 * self._fes + (self._pes if potential else 0) +
+                                            (8 if self.cfg.flow else 0))
         paired = self.ring == "seamless" and self.with_potential
         if tuning is not None:
             self._apply_tuning(tuning)
@@ -144,6 +158,8 @@ class FFMPVec:
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
+    OBS_FORMATS = {"f32": (_abi.OBS_F32, torch.float32, torch.float32),
+                   "u8f16": (_abi.OBS_U8F16, torch.uint8, torch.float16)}
     _ARENA_ALIGN = 2 << 20
     WINDOW_DEFAULT = 8
     WINDOW_HBM_FRACTION = 0.6  # auto window: frames + other planes within this share of free HBM
@@ -154,10 +170,11 @@ class FFMPVec:
                 raise ValueError("frame_window must be >= 2")
             return int(w)
         cfg, N = self.cfg, self.num_envs
-        plane = N * cfg.grid * cfg.grid * 4
-        if plane * 3 < self.AUTOTUNE_MIN_BYTES:
+        G2 = cfg.grid * cfg.grid
+        plane = N * G2 * self._fes
+        if N * G2 * 12 < self.AUTOTUNE_MIN_BYTES:  # (the f32 layout's bytes: same choice for both formats)
             return 2
-        other = plane * ((1 if self.with_potential else 0) + (2 if cfg.flow else 0))
+        other = N * G2 * ((self._pes if self.with_potential else 0) + (8 if cfg.flow else 0))
         free, _ = torch.cuda.mem_get_info(self.device)
         budget = self.WINDOW_HBM_FRACTION * free - other
         return int(max(2, min(self.WINDOW_DEFAULT, budget // plane)))
@@ -169,8 +186,9 @@ class FFMPVec:
         f32, f64, i32, b = torch.float32, torch.float64, torch.int32, torch.bool
         specs = [
             # observation planes first: the big, hot, write-streamed buffers
-            ("frames", (N, 2, G, G) if self.frame_window == 2 else (self.frame_window, N, G, G), f32),
-            ("potential", (N, G, G), f32),
+            ("frames", (N, 2, G, G) if self.frame_window == 2 else (self.frame_window, N, G, G),
+             self._frame_dtype),
+            ("potential", (N, G, G), self._pot_dtype),
             ("flow", (N, 2, G, G), f32),
             # state
             ("pose", (N, 3), f64), ("goal", (N, 2), f64), ("d0", (N,), f64),
@@ -205,7 +223,8 @@ class FFMPVec:
         torch.cuda.synchronize(self.device)  # the pairing probes write the potential plane on their own stream
         try:
             partner = self.potential if self.PAIR_SLOTS else None
-            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, partner=partner)
+            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, bits=8 * self._fes,
+                                           partner=partner)
             self.frames = self._ring.tensor
             self.ring_meta = self._ring.info()
         except _abi.FFMPBackendError:
@@ -421,8 +440,8 @@ class FFMPVec:
         once, and the potential plane streams beside each slot at its own rate (one slow
         slot/plane pairing makes one step in W ~25 % slower, profiles/r01_ring.txt §6), so a
         placement check must see all of them."""
-        plane_bytes = self.state_m.numel() * 4 * ((1.5 if self.with_potential else 1.0) +
-                                                 (1.0 if self.flow is not None else 0.0))
+        plane_bytes = self.state_m.numel() * (self._fes + (self._pes / 2 if self.with_potential else 0.0) +
+                                              (4.0 if self.flow is not None else 0.0))
         steps = 3 if plane_bytes >= (8 << 30) else 12
         cyc = {"wrap": self.frame_window - 1, "seamless": self.frame_window}.get(self.ring, 1)
         return -(-steps // cyc) * cyc
@@ -481,13 +500,31 @@ class FFMPVec:
         _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE2, _abi.RASTER_NT | _abi.RASTER_TILE8,
     )
 
+    # The compact format (obs_format="u8f16") writes 3 bytes per cell and is bound by the per-task
+    # cull / wall / index work rather than by HBM (tools/compact_probe.py): 16 cells per lane
+    # (1024-cell wave tasks) by default, tiles R x 1024/R; NARROW = the 4-cells-per-lane kernel.
+    COMPACT_SHAPES = (
+        (16384, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW), (16384, _abi.RASTER_NT | _abi.RASTER_TILE16),
+        (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (16384, _abi.RASTER_NT | _abi.RASTER_TILE4),
+        (8192, _abi.RASTER_NT | _abi.RASTER_TILE16), (32768, _abi.RASTER_NT | _abi.RASTER_TILE16),
+        (16384, _abi.RASTER_PLAIN | _abi.RASTER_TILE16), (16384, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE16),
+        (16384, _abi.RASTER_NT), (8192, _abi.RASTER_NT | _abi.RASTER_TILE8),
+    )
+    COMPACT_FUSED_FLAGS = (
+        _abi.RASTER_NT | _abi.RASTER_TILE16, _abi.RASTER_NT | _abi.RASTER_TILE8, _abi.RASTER_NT | _abi.RASTER_TILE4,
+        _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW, _abi.RASTER_PLAIN | _abi.RASTER_TILE16,
+        _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE16, _abi.RASTER_NT,
+    )
+
     XCD_SHAPES = True  # autotune candidates include the XCD-aware block remap
 
     def _shape_candidates(self):
-        return [sh for sh in self.RASTER_SHAPES if self.XCD_SHAPES or not sh[1] & _abi.RASTER_XCD]
+        shapes = self.COMPACT_SHAPES if self.obs_format == "u8f16" else self.RASTER_SHAPES
+        return [sh for sh in shapes if self.XCD_SHAPES or not sh[1] & _abi.RASTER_XCD]
 
     def _fused_candidates(self):
-        return [f for f in self.FUSED_FLAGS if self.XCD_SHAPES or not f & _abi.RASTER_XCD]
+        flags = self.COMPACT_FUSED_FLAGS if self.obs_format == "u8f16" else self.FUSED_FLAGS
+        return [f for f in flags if self.XCD_SHAPES or not f & _abi.RASTER_XCD]
 
     def _tune_fused(self, steps: int) -> Optional[dict]:
         """Time whole steps of the two-launch path (the tuned raster shapes) against the fused
@@ -526,7 +563,7 @@ class FFMPVec:
         G2 = self.cfg.grid * self.cfg.grid
         self._obs_c = _abi.ObsT(self.state_m.data_ptr(), self.state_g.data_ptr(), self.state_v.data_ptr(),
                                 self.state_t.data_ptr(), _ptr(self.potential), self.grad.data_ptr(),
-                                _ptr(self.lidar), _ptr(self.flow), *self._sm_strides())
+                                _ptr(self.lidar), _ptr(self.flow), *self._sm_strides(), self._fmt)
         self._out_c = _abi.OutT(self.reward.data_ptr(), self.done.data_ptr(), self.is_goal.data_ptr(),
                                 self.collision.data_ptr(), self.truncated.data_ptr())
         self._build_slices()
@@ -550,7 +587,8 @@ class FFMPVec:
                              off(self.obst_r, a), off(self.t, a), off(self.episode, a), off(self.record, a),
                              self.err.data_ptr(), off(self.term_record, a), off(self.term_obs, a))
             ob = _abi.ObsT(off(self.state_m, a), off(self.state_g, a), off(self.state_v, a), off(self.state_t, a),
-                           off(self.potential, a), off(self.grad, a), off(self.lidar, a), off(self.flow, a))
+                           off(self.potential, a), off(self.grad, a), off(self.lidar, a), off(self.flow, a), 0, 0,
+                           self._fmt)
             out = _abi.OutT(off(self.reward, a), off(self.done, a), off(self.is_goal, a), off(self.collision, a),
                             off(self.truncated, a))
             self._slices.append((a, n, st, ob, out, off(self.record, a)))
@@ -572,7 +610,7 @@ class FFMPVec:
         return self.frames[self._wpos:self._wpos + 2].transpose(0, 1)
 
     def _sm_strides(self):
-        """(env stride, frame stride) of state_m in floats, for ffmp_obs_t."""
+        """(env stride, frame stride) of state_m in elements, for ffmp_obs_t."""
         G2 = self.cfg.grid * self.cfg.grid
         if self.frame_window == 2:
             return (2 * G2, G2)
@@ -580,13 +618,13 @@ class FFMPVec:
 
     def _set_window(self, p: int) -> None:
         self._wpos = p
-        self._obs_c.state_m = self.frames.data_ptr() + p * self.frames.stride(0) * 4
+        self._obs_c.state_m = self.frames.data_ptr() + p * self.frames.stride(0) * self._fes
 
     def _raster_bytes(self, n: int, full: bool) -> int:
         """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs
-        reset during a newest-only launch: 4 G^2 each, added by bench.py from the episode counts)."""
+        reset during a newest-only launch: one frame each, added by bench.py from the episode counts)."""
         G2 = self.cfg.grid * self.cfg.grid
-        per = (8 if full else 4) * G2 + (4 * G2 if self.potential is not None else 0) + \
+        per = (2 if full else 1) * self._fes * G2 + (self._pes * G2 if self.potential is not None else 0) + \
             (8 * G2 if self.flow is not None else 0) + 4 * self.cfg.record_len()
         return n * per
 
@@ -773,18 +811,19 @@ class FFMPVec:
         G, L = self.cfg.grid, self.cfg.n_beams
         inf = np.inf
 
-        def box(lo, hi, shape):
-            lo = np.broadcast_to(np.asarray(lo, dtype=np.float32), lead + shape)
-            hi = np.broadcast_to(np.asarray(hi, dtype=np.float32), lead + shape)
-            return Box(lo, hi, dtype=np.float32)
+        def box(lo, hi, shape, dtype=np.float32):
+            lo = np.broadcast_to(np.asarray(lo, dtype=dtype), lead + shape)
+            hi = np.broadcast_to(np.asarray(hi, dtype=dtype), lead + shape)
+            return Box(lo, hi, dtype=dtype)
 
-        sp = {"state_m": box(0.0, 255.0, (2, G, G)),
+        compact = self.obs_format == "u8f16"
+        sp = {"state_m": box(0, 255, (2, G, G), np.uint8) if compact else box(0.0, 255.0, (2, G, G)),
               "state_g": box([0.0, -np.pi], [inf, np.pi], (2,)),   # [dist, orient]
               "state_v": box([0.0, -np.pi], [inf, np.pi], (2,)),   # [|dxy|, wrap(dyaw)] per step
               "state_t": box(0.0, inf, (1,)),
               "grad": box(-inf, inf, (2,))}
         if self.potential is not None:
-            sp["potential"] = box(0.0, inf, (G, G))
+            sp["potential"] = box(0.0, inf, (G, G), np.float16 if compact else np.float32)
         if L:
             sp["lidar"] = box(-inf, inf, (L,))
         if self.flow is not None:
@@ -850,7 +889,7 @@ class FFMPVec:
 
     def hbm_bytes(self) -> int:
         if self._arena_buf is not None:
-            ring = self.frame_window * self.frames.stride(0) * 4 if self.ring == "seamless" else 0
+            ring = self.frame_window * self.frames.stride(0) * self._fes if self.ring == "seamless" else 0
             return self._arena_buf.numel() + ring
         return sum(t.numel() * t.element_size() for t in vars(self).values() if isinstance(t, torch.Tensor))
 
@@ -858,7 +897,7 @@ class FFMPVec:
         c = self.cfg
         return (f"FFMPVec(num_envs={self.num_envs}, G={c.grid}, K={c.n_obst}, L={c.n_beams}, "
                 f"moving={c.moving}, device={self.device}, env_offset={self.env_offset}, "
-                f"frame_window={self.frame_window}, ring={self.ring})")
+                f"frame_window={self.frame_window}, ring={self.ring}, obs_format={self.obs_format})")
 
 
 __all__ = ["FFMPVec", "PRESETS"]

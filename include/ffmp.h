@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 3
+#define FFMP_ABI_VERSION 4
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -122,6 +122,15 @@ typedef struct ffmp_state {
   float* term_obs;    /* (N, 5) state_g[2], state_v[2], state_t */
 } ffmp_state_t;
 
+/* Observation plane formats (ffmp_obs_t.format).  F32: the reference consumer layout
+ * (train.py:543-545 state_m float32 0/255; potential float32).  U8F16: a compact layout for
+ * consumers that convert on load — state_m frames as uint8 0/255 (the same values) and the
+ * potential plane as IEEE binary16 (float32 value rounded to nearest even); the state_m and
+ * potential pointers then address uint8_t / binary16 elements and the state_m strides count
+ * elements.  3 instead of 8 bytes per cell of a newest-only raster.  No flow planes. */
+#define FFMP_OBS_F32 0
+#define FFMP_OBS_U8F16 1
+
 /* Observation tensors (device pointers).  Layout = reference train.py:44,543-557
  * with a leading N: state_m (N,2,G,G) [older, newest] values 0/255 as float. */
 typedef struct ffmp_obs {
@@ -134,11 +143,13 @@ typedef struct ffmp_obs {
   float* lidar;     /* (N,L) ranges (+inf = no return, -inf = inside), NULL if L == 0 */
   float* flow;      /* (N,2,G,G) ego-frame velocity (m/s) of the disc covering each cell of the
                        newest frame (lowest disc index wins), 0 elsewhere; NULL unless cfg.flow */
-  int64_t state_m_stride;       /* floats from env e's older frame to env e+1's; 0 = 2*G*G */
+  int64_t state_m_stride;       /* elements (floats) from env e's older frame to env e+1's; 0 = 2*G*G */
   int64_t state_m_frame_stride; /* floats from env e's older frame to its newest; 0 = G*G.
                                    0/0 is the contiguous (N,2,G,G) layout.  A slot-major frame
                                    window (W, N, G, G) uses G*G / N*G*G with state_m at the
                                    older slot (see FFMP_RASTER_NEWEST). */
+  int32_t format;   /* FFMP_OBS_F32 (0) or FFMP_OBS_U8F16 */
+  int32_t reserved;
 } ffmp_obs_t;
 
 /* Per-step outputs (device pointers, N each). Flags are 0/1 bytes. */
@@ -156,7 +167,8 @@ const char* ffmp_last_error(void);
 /* Layout check for FFI bindings: which = 0 sizeof(ffmp_cfg_t), 1 sizeof(ffmp_state_t),
  * 2 sizeof(ffmp_obs_t), 3 sizeof(ffmp_out_t), 4 offsetof(ffmp_cfg_t, res),
  * 5 offsetof(ffmp_cfg_t, res_f), 6 offsetof(ffmp_cfg_t, seed),
- * 7 offsetof(ffmp_cfg_t, beam_cs), 8 sizeof(ffmp_episode_t); -1 otherwise. */
+ * 7 offsetof(ffmp_cfg_t, beam_cs), 8 sizeof(ffmp_episode_t),
+ * 9 offsetof(ffmp_obs_t, format); -1 otherwise. */
 int64_t ffmp_layout(int32_t which);
 
 /* Launch-shape tuning (process-wide; not thread-safe against concurrent launches).
@@ -211,7 +223,11 @@ int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
 #define FFMP_RASTER_TILE4 32 /* 4 x 64-cell tile (compact cull box: fewer discs per task)       */
 #define FFMP_RASTER_TILE8 64 /* 8 x 32-cell tile; any TILE flag needs G % (256/R) == 0 and blocks
                                 of whole R-row bands (cells_per_block % (G*R) == 0 or >= G*G),
-                                else the 256-cell chunks are used */
+                                else the 256-cell chunks are used.  With FFMP_OBS_U8F16 and
+                                G % 16 == 0 a wave task is 1024 cells (16 per lane): tiles are
+                                R x 1024/R cells and need G % (1024/R) == 0 */
+#define FFMP_RASTER_TILE16 256 /* 16 x 16-cell tile (compact 16 cells per lane: 16 x 64) */
+#define FFMP_RASTER_NARROW 128 /* FFMP_OBS_U8F16: keep 4 cells per lane (256-cell wave tasks) */
 int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                    const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
                    int32_t flags, void* stream);
@@ -331,7 +347,7 @@ int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partn
 int ffmp_ring_destroy(ffmp_ring_t* ring);
 int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap);
 int64_t ffmp_ring_pool_bytes(int32_t device);
-/* A dlpack.h (v0.8) DLManagedTensor* of float `bits` elements over `data` (element strides,
+/* A dlpack.h (v0.8) DLManagedTensor* of `bits` elements (8: uint8, 16/32/64: float) over `data` (element strides,
  * ndim <= 8), for consumers that take DLPack (torch.utils.dlpack.from_dlpack, CuPy, JAX).
  * Its deleter frees it and, when `owner` is a ring, drops the reference it took on it: a ring
  * is parked once ffmp_ring_destroy was called AND every such tensor was deleted.

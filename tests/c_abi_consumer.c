@@ -83,7 +83,8 @@ int main(void) {
   float* frames = (float*)dalloc((size_t)W * N * G2 * 4);
   ffmp_obs_t ob = {frames, (float*)dalloc(N * 2 * 4), (float*)dalloc(N * 2 * 4),
                    (float*)dalloc(N * 4), (float*)dalloc(N * G2 * 4), (float*)dalloc(N * 2 * 4),
-                   (float*)dalloc(N * L * 4), NULL, (int64_t)G2, (int64_t)N * (int64_t)G2};
+                   (float*)dalloc(N * L * 4), NULL, (int64_t)G2, (int64_t)N * (int64_t)G2,
+                   FFMP_OBS_F32, 0};
   ffmp_out_t out = {(float*)dalloc(N * 4), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N), (uint8_t*)dalloc(N),
                     (uint8_t*)dalloc(N)};
   int64_t* act = (int64_t*)dalloc(N * 8);

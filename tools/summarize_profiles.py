@@ -64,7 +64,7 @@ def per_launch(vals, key, k):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    cfg = sys.argv[2] if len(sys.argv) > 2 else "C3"
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "C3"  # label: <workload>[_u8f16]
     os.makedirs(OUT, exist_ok=True)
     stats = find(f"trace_{cfg}/**/run_kernel_stats.csv") or find("run_kernel_stats.csv")
     if stats:
@@ -92,6 +92,7 @@ def main():
         pm["frame_window"] = bj["config"].get("frame_window", 2)
         pm["ring"] = bj["config"].get("ring", "wrap" if pm["frame_window"] > 2 else "contiguous")
         pm["fused"] = bool(bj["config"].get("fused", False))
+        pm["obs_format"] = bj["config"].get("obs_format", "f32")
         pm["timed_kernel"] = bj["roofline"].get("kernel", "raster_kernel")
         pm["raster_algorithmic_bytes_per_launch"] = alg
         if "raster_kernel" in pm["kernels"]:
@@ -99,6 +100,7 @@ def main():
             pm["raster_traffic_over_algorithmic"] = hb / alg
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
                 json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
+                           "obs_format": bj["config"].get("obs_format", "f32"),
                            "raster_hbm_bytes_per_launch": hb,
                            "source": f"{tag}_{cfg}_pmc.json"}, f, indent=1)
     trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")

@@ -136,7 +136,10 @@ def cpu_baseline_parallel(cfg, seconds: float, procs: int):
 
 def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):
     """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}{'' if obs_format == 'f32' else '_' + obs_format}.json")
+    label = f"{workload}{'' if obs_format == 'f32' else '_' + obs_format}"
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{'_fused' if fused else ''}.json")
+    if not os.path.exists(path):  # the one-launch and two-launch steps are profiled separately
+        path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}.json")
     if not os.path.exists(path):
         return None
     try:

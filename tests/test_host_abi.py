@@ -2,6 +2,7 @@
 include/ffmp.h declares, its struct layout matches the ctypes binding, and the
 host-side entry points / argument validation behave (no kernel is launched)."""
 import ctypes as C
+import json
 import math
 import os
 import re
@@ -145,6 +146,32 @@ def test_bytes_model():
     assert bytes_per_env_step(preset("C3"), window=8, seamless=True)["raster"] == 8 * 65536 + 4 * (16 + 12 * 16)
     assert bytes_per_env_step(preset("C3"), window=2, seamless=True)["raster"] == b["raster"]
     assert b["total"] > b["raster"]
+    # compact format: 1-byte frames, 2-byte potential
+    assert bytes_per_env_step(preset("C3"), window=8, seamless=True, obs_format="u8f16")["raster"] == \
+        3 * 65536 + 4 * (16 + 12 * 16)
+    assert bytes_per_env_step(preset("C3"), obs_format="u8f16")["raster"] == 4 * 65536 + 4 * (16 + 12 * 16)
+
+
+def test_bench_traffic_lookup():
+    """bench.py reads roofline.traffic from the committed PMC summary of the same configuration
+    (step kind, frame window, ring, obs format), else reports null."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(HEADER), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    prof = os.path.join(os.path.dirname(HEADER), "..", "profiles")
+    for name, fused, fmt in (("C3", False, "f32"), ("C3", True, "f32"), ("C3", False, "u8f16")):
+        label = name + ("" if fmt == "f32" else "_" + fmt) + ("_fused" if fused else "")
+        path = os.path.join(prof, f"pmc_traffic_{label}.json")
+        if not os.path.exists(path):
+            continue
+        d = json.load(open(path))
+        got = bench.load_traffic(name, d["n_envs"], d["frame_window"], d["ring"], fused, fmt)
+        assert got == d["raster_hbm_bytes_per_launch"]
+        assert bench.load_traffic(name, d["n_envs"] + 1, d["frame_window"], d["ring"], fused, fmt) is None
+        assert bench.load_traffic(name, d["n_envs"], d["frame_window"] + 1, d["ring"], fused, fmt) is None
+    assert bench.load_traffic("C3", 32768, 8, "seamless", False, "u8f16") != bench.load_traffic("C3", 32768, 8,
+                                                                                               "seamless", False)
 
 
 def test_missing_library_fails_loudly(tmp_path):

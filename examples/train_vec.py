@@ -40,13 +40,15 @@ def main():
     ap.add_argument("--target-every", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--save", default="")
+    ap.add_argument("--obs-format", default="f32", choices=["f32", "u8f16"],
+                    help="u8f16: uint8 state_m / float16 potential (the Brain converts on input)")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
 
     dev = torch.device("cuda:0")
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed)
-    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True)
+    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed)
     obs = env.reset()
     tracker = EpisodeTracker(args.envs, device=dev)

@@ -205,12 +205,33 @@ FFMP_DEV float rep_reach2(const ffmp_cfg_t& cfg, float r) {
   return (a * a) * 1.000004f;  // > ((rho0 + r)(1 + 2^-20))^2 despite the rounding of a, a*a and the product
 }
 
+// Correctly rounded float32 sqrt for 2^-96 <= s < inf: v_sqrt_f32 (faithful) then the
+// neighbour-residual correction — sqrtf without its tiny-input scaling and special-value
+// select (16 -> 8 VALU).  Below 2^-96 it may differ from sqrtf, but add_repulsive_s only feeds
+// it into fmaxf(sqrt(s) - r, rho_min) with r >= 0 and rho_min >= 2^-48, where both give rho_min.
+FFMP_DEV float sqrt_rn(float s) {
+  const float y = __builtin_amdgcn_sqrtf(s);
+  const float yd = __int_as_float(__float_as_int(y) - 1), yu = __int_as_float(__float_as_int(y) + 1);
+  const float rd = __builtin_fmaf(-yd, y, s), ru = __builtin_fmaf(-yu, y, s);
+  const float t = (rd <= 0.0f) ? yd : y;
+  return (ru > 0.0f) ? yu : t;
+}
+
+// Correctly rounded float32 1/d for normal d with 1/d normal: v_rcp_f32 (1 ulp) and one FMA
+// Newton step (11 -> 3 VALU).  Both helpers are checked bit-for-bit against sqrtf / 1.0f/d
+// over every float of their ranges by ffmp_check_exact_math (tests/test_gpu_exact_math.py).
+FFMP_DEV float rcp_rn(float d) {
+  const float y = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+}
+
 FFMP_DEV float add_repulsive_s(const ffmp_cfg_t& cfg, float U, float s, float r, float reach2) {
   if (s >= reach2) return U;
-  float d = sqrtf(s) - r;
+  float d = sqrt_rn(s) - r;
   d = fmaxf(d, cfg.rho_min_f);
   if (d < cfg.rho0_f) {
-    const float q = 1.0f / d - cfg.inv_rho0_f;
+    const float q = rcp_rn(d) - cfg.inv_rho0_f;
     U = U + cfg.half_kr_f * (q * q);
   }
   return U;

@@ -65,6 +65,10 @@ int check_cfg(const ffmp_cfg_t* c) {
   if (c->n_foot < 0 || c->n_foot > FFMP_MAX_FOOT)
     return fail(FFMP_E_CFG, "n_foot out of range: %d", c->n_foot);
   if (c->n_beams > 0 && !c->beam_cs) return fail(FFMP_E_CFG, "beam_cs is NULL with n_beams > 0");
+  // the raster's sqrt_rn / rcp_rn are exact on this domain (ffmp_device.h)
+  if (!(c->rho_min_f >= 0x1p-48f && c->rho_min_f <= 0x1p100f) || !(c->rho0_f <= 0x1p100f))
+    return fail(FFMP_E_CFG, "rho_min must lie in [2^-48, 2^100] and rho0 <= 2^100");
+  if (!(c->obst_rmin >= 0.0)) return fail(FFMP_E_CFG, "obst_rmin must be >= 0");
   for (int f = 0; f < c->n_foot; ++f) {
     const int i = c->grid / 2 + c->foot_di[f], j = c->grid / 2 + c->foot_dj[f];
     if (i < 0 || j < 0 || i >= c->grid || j >= c->grid)
@@ -824,6 +828,24 @@ int scan_impl(int64_t n, int32_t L, const T* ranges, double thr, uint8_t* collid
 // Episode bookkeeping (src/train.py:501-505, 579-587, 593, 607, 611-682), one thread per env.
 // Counts for totals[] are wave ballots: one atomic per counter per wave.
 // ============================================================================
+// ============================================================================
+// Exhaustive check of the raster's sqrt_rn / rcp_rn against the IEEE sqrtf and 1.0f / d over the
+// float bit patterns [lo, hi) (grid-stride; one global atomic per mismatching wave).
+// ============================================================================
+__global__ __launch_bounds__(256) void exact_math_kernel(int32_t which, uint32_t lo, uint32_t hi,
+                                                          unsigned long long* mismatches, uint32_t* first_bits) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < hi; b += stride) {
+    const float x = __uint_as_float((uint32_t)b);
+    const float fast = which == 0 ? sqrt_rn(x) : rcp_rn(x);
+    const float ieee = which == 0 ? sqrtf(x) : 1.0f / x;
+    const bool bad = __float_as_uint(fast) != __float_as_uint(ieee);
+    const unsigned long long m = __ballot(bad);
+    if (bad && (int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicMin(first_bits, (uint32_t)b);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(mismatches, (unsigned long long)__popcll(m));
+  }
+}
+
 __device__ __forceinline__ void wave_count(uint64_t* totals, int k, bool pred) {
   const unsigned long long m = __ballot(pred);
   if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long*)&totals[k], (unsigned long long)__popcll(m));
@@ -1255,6 +1277,18 @@ int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr, u
 int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr, uint8_t* collide,
                             double* min_r, void* stream) {
   return scan_impl<double>(n, L, ranges, thr, collide, min_r, stream);
+}
+
+int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches,
+                          uint32_t* first_bits, void* stream) {
+  if (which != 0 && which != 1) return fail(FFMP_E_ARG, "which must be 0 (sqrt) or 1 (rcp), got %d", which);
+  if (!mismatches || !first_bits) return fail(FFMP_E_ARG, "mismatches/first_bits is NULL");
+  if (hi_bits <= lo_bits) return FFMP_OK;
+  const uint64_t n = (uint64_t)hi_bits - lo_bits;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(exact_math_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, which, lo_bits, hi_bits,
+                     mismatches, first_bits);
+  return check_launch("ffmp_check_exact_math");
 }
 
 int ffmp_episode_init(int64_t n, const uint8_t* mask, int32_t flags, ffmp_episode_t* ep, void* stream) {

@@ -271,6 +271,13 @@ int ffmp_scan_collision(int64_t n, int32_t L, const float* ranges, double thr,
 int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double thr,
                             uint8_t* collide, double* min_r, void* stream);
 
+/* Self-check of the raster's exact fast math (no reference counterpart: the potential plane is
+ * [no reference]): which = 0 compares sqrt_rn with sqrtf, 1 compares rcp_rn with
+ * 1.0f / d, over the float bit patterns [lo_bits, hi_bits).  Adds the mismatch count to
+ * *mismatches and atomic-mins the first mismatching pattern into *first_bits (device memory). */
+int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits,
+                          unsigned long long* mismatches, uint32_t* first_bits, void* stream);
+
 /* Episode bookkeeping of the training loop, batched (one record per env, device memory).
  * Per env and per ffmp_episode_update, exactly as src/train.py:579-682 does per iteration:
  *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)

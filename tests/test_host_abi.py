@@ -239,3 +239,17 @@ def test_ring_api_without_gpu(lib):
     assert lib.ffmp_ring_pool_bytes(-1) == 0
     info = (C.c_double * 5)()
     assert lib.ffmp_ring_info(None, info, 5) == -1
+
+
+def test_exact_math_domain_validation_no_gpu(lib):
+    """The raster's sqrt_rn / rcp_rn are exact on rho_min in [2^-48, 2^100], obst_rmin >= 0
+    (ffmp_device.h); check_cfg refuses configurations outside that domain before any launch."""
+    ob = _abi.ObsT()
+    for field, val in (("rho_min_f", 0.0), ("rho_min_f", 2.0 ** -60), ("rho0_f", float("inf")),
+                       ("rho_min_f", float("nan")), ("obst_rmin", -0.1)):
+        bad = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=0))
+        setattr(bad, field, val)
+        assert lib.ffmp_raster(C.byref(bad), 1, None, None, C.byref(ob), None) == -3, field
+    assert b"rho" in lib.ffmp_last_error() or b"obst_rmin" in lib.ffmp_last_error()
+    assert lib.ffmp_check_exact_math(2, 0, 1, None, None, None) == -1
+    assert lib.ffmp_check_exact_math(0, 0, 1, None, None, None) == -1

@@ -399,10 +399,16 @@ class FFMPVec:
             self.step(a, timing=t)
         torch.cuda.synchronize(self.device)
         per: Dict[int, list] = {}
-        for k, r in enumerate(t):  # step k after a reset writes virtual slot k+1 -> physical (k+1) % W
-            per.setdefault((k + 1) % W, []).append(r[0].elapsed_time(r[1]))
+        for k, r in enumerate(t):
+            per.setdefault(self._slot_written(k), []).append(r[0].elapsed_time(r[1]))
         self._clear_after_tuning()
         return {i: float(np.median(v)) for i, v in per.items()}
+
+    def _slot_written(self, k: int) -> int:
+        """Physical ring slot whose newest frame step k (0-based) after a full reset writes: the
+        reset leaves the window at [0, 1], step k slides it to [k+1, k+2] and writes the newest
+        frame, virtual slot k+2 -> physical (k+2) % W (virtual slot W is slot 0)."""
+        return (k + 2) % self.frame_window
 
     def _repair_slots(self) -> None:
         history = []

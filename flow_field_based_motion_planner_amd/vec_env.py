@@ -386,7 +386,7 @@ class FFMPVec:
     # newest-only raster over two ring cycles and rebuild the ring with new pieces for slots
     # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.
     SLOW_SLOT = 1.06
-    REPAIR_ROUNDS = 1
+    REPAIR_ROUNDS = 2
     PAIR_SLOTS = True  # build the ring's slots from pieces probed against the potential plane
 
     def _slot_ms(self) -> Dict[int, float]:

@@ -384,8 +384,9 @@ class FFMPVec:
     # Slot repair (seamless ring).  The pairing probe at ring creation predicts most, not all,
     # slow slot/potential pairings; the step loop itself is the judge: time every slot's
     # newest-only raster over two ring cycles and rebuild the ring with new pieces for slots
-    # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.
-    SLOW_SLOT = 1.06
+    # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.  A
+    # rebuild re-maps every slot, so only clearly slow slots are worth one.
+    SLOW_SLOT = 1.12
     REPAIR_ROUNDS = 2
     PAIR_SLOTS = True  # build the ring's slots from pieces probed against the potential plane
 

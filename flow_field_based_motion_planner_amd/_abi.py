@@ -255,6 +255,8 @@ class SeamlessRing:
         self.handle = None
         self.tensor = None
         self.rebuilds = 0
+        self.reverts = 0
+        self._prev = None  # (handle, tensor, slot_stride) of the ring before an undecided rebuild
         self._adopt(ring, base, stride)
 
     @staticmethod
@@ -263,9 +265,10 @@ class SeamlessRing:
             return None, 0
         return partner.data_ptr(), partner.numel() * partner.element_size()
 
-    def _adopt(self, ring, base, stride, zero: bool = True) -> None:
+    def _adopt(self, ring, base, stride, zero: bool = True, keep_old: bool = False) -> None:
         """Wrap a fresh ring as the (slots + 1, *plane) tensor (zeroed unless `zero` is False);
-        this object keeps the creator's reference (the handle) so the ring can be rebuilt."""
+        this object keeps the creator's reference (the handle) so the ring can be rebuilt.
+        keep_old: the previous ring stays alive (revert() / drop_previous())."""
         esize = self.bits // 8
         try:
             inner = [1]
@@ -279,30 +282,55 @@ class SeamlessRing:
         except Exception:
             self.lib.ffmp_ring_destroy(ring)
             raise
-        old = self.handle
+        self.drop_previous()
+        old = (self.handle, self.tensor, getattr(self, "slot_stride", None))
         self.handle, self.tensor, self.slot_stride = ring.value, t, stride.value
-        if old is not None:
-            self.lib.ffmp_ring_destroy(C.c_void_p(old))
+        if keep_old:
+            self._prev = old
+        elif old[0] is not None:
+            self.lib.ffmp_ring_destroy(C.c_void_p(old[0]))
 
-    def rebuild(self, slot_mask: int, partner=None) -> None:
+    def rebuild(self, slot_mask: int, partner=None, keep_old: bool = False) -> None:
         """Replace the pieces of the slots in slot_mask (ffmp_ring_rebuild); `tensor` becomes a new
-        tensor — views of the old one must not be used any more.  Kept slots keep their bytes,
-        replaced ones are undefined."""
+        tensor — views of the old one must not be used any more.  Kept slots keep their bytes
+        (the same memory as the old ring's), replaced ones are undefined.  keep_old: the old ring
+        stays alive until drop_previous() (keep the new one) or revert() (back to the old one),
+        so that a caller can time both."""
         ring, base, stride = _P(), _P(), _I64()
         pp, pb = self._partner(partner)
         check(self.lib.ffmp_ring_rebuild(C.c_void_p(self.handle), int(slot_mask), pp, pb, C.byref(ring),
                                          C.byref(base), C.byref(stride)), "ffmp_ring_rebuild")
         self.rebuilds += 1
-        self._adopt(ring, base, stride, zero=False)
+        self._adopt(ring, base, stride, zero=False, keep_old=keep_old)
+
+    def drop_previous(self) -> None:
+        """Keep the current ring: release the one an undecided rebuild(keep_old=True) replaced."""
+        prev, self._prev = self._prev, None
+        if prev is not None:
+            self.lib.ffmp_ring_destroy(C.c_void_p(prev[0]))
+
+    def revert(self) -> None:
+        """Undo the last rebuild(keep_old=True): the previous ring (and its tensor) is current
+        again; the rebuilt one is released (its new pieces return to the pool once every view of
+        its tensor is gone)."""
+        if self._prev is None:
+            raise RuntimeError("SeamlessRing.revert: no rebuild to undo")
+        cur = self.handle
+        self.handle, self.tensor, self.slot_stride = self._prev
+        self._prev = None
+        self.reverts += 1
+        self.lib.ffmp_ring_destroy(C.c_void_p(cur))
 
     def info(self) -> dict:
         out = (C.c_double * 5)()
         self.lib.ffmp_ring_info(C.c_void_p(self.handle), out, 5)
         return {"pieces": int(out[0]), "pieces_new": int(out[1]), "pair_probes": int(out[2]),
-                "pair_gbs_min": round(out[3], 1), "pair_gbs_max": round(out[4], 1), "rebuilds": self.rebuilds}
+                "pair_gbs_min": round(out[3], 1), "pair_gbs_max": round(out[4], 1), "rebuilds": self.rebuilds,
+                "reverts": self.reverts}
 
     def __del__(self):
         try:
+            self.drop_previous()
             if self.handle is not None:
                 self.lib.ffmp_ring_destroy(C.c_void_p(self.handle))
                 self.handle = None

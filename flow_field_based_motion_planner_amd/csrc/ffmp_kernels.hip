@@ -1147,7 +1147,9 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   const bool ct = obs->format == FFMP_OBS_U8F16;
   const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
   const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
-  if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
+  const int64_t sm_frame_abs = sm_frame < 0 ? -sm_frame : sm_frame;  // negative: newest in a lower slot
+  if (sm_stride < (int64_t)G2 || sm_frame_abs < (int64_t)G2 ||
+      (sm_stride < 2 * (int64_t)G2 && sm_frame_abs < n * (int64_t)G2))
     return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld elements (G*G = %d)",
                 (long long)sm_stride, (long long)sm_frame, G2);
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
@@ -1219,7 +1221,9 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
   const int G2 = cfg->grid * cfg->grid;
   const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
   const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
-  if (sm_stride < (int64_t)G2 || sm_frame < (int64_t)G2 || (sm_stride < 2 * (int64_t)G2 && sm_frame < n * (int64_t)G2))
+  const int64_t sm_frame_abs = sm_frame < 0 ? -sm_frame : sm_frame;  // negative: newest in a lower slot
+  if (sm_stride < (int64_t)G2 || sm_frame_abs < (int64_t)G2 ||
+      (sm_stride < 2 * (int64_t)G2 && sm_frame_abs < n * (int64_t)G2))
     return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld elements (G*G = %d)", (long long)sm_stride,
                 (long long)sm_frame, G2);
   const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);

@@ -136,10 +136,12 @@ class FFMPVec:
             raise ValueError("pipeline > 1 and fused=True are exclusive")
         if self.pipeline_slices > 1:
             self._fused_req = False
-        self._build_structs()
         plane_bytes = self.num_envs * G2 * (2 * self._fes + (self._pes if potential else 0) +
                                             (8 if self.cfg.flow else 0))
         paired = self.ring == "seamless" and self.with_potential
+        if paired and plane_bytes >= self.REPLACE_MIN_BYTES and (tuning is not None or autotune):
+            self._relocate_partner()
+        self._build_structs()
         if tuning is not None:
             self._apply_tuning(tuning)
             if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
@@ -411,19 +413,98 @@ class FFMPVec:
         frame, virtual slot k+2 -> physical (k+2) % W (virtual slot W is slot 0)."""
         return (k + 2) % self.frame_window
 
+    # Partner relocation (seamless ring).  The ring's pieces are probed against the potential
+    # plane; when no probe reaches PAIR_FAST_GBS the plane itself sits where nothing pairs well
+    # (round-1 C5 and some C3 boxes: every probe 4.9-5.5 TB/s).  Then the arena (with the potential
+    # plane) is allocated again elsewhere — the earlier arenas and a growing spacer stay held so
+    # the allocator must return different memory — and a ring is paired against the new plane
+    # (the losing rings' pieces return to the pool and are probed again first); the pair with the
+    # fastest probe is kept.
+    PAIR_FAST_GBS = 6200.0  # ffmp_ring.hip kPairFastGBs
+    PARTNER_TRIES = 3
+
+    def _relocate_partner(self) -> None:
+        meta = self.ring_meta or {}
+        if not meta.get("pair_probes") or meta.get("pair_gbs_max", 0.0) >= self.PAIR_FAST_GBS:
+            return
+        names = [n for n, _, _ in self._buffer_specs(with_frames=False)]
+
+        def snap():
+            return {"gbs": self.ring_meta["pair_gbs_max"], "arena": self._arena_buf, "ring": self._ring,
+                    "meta": self.ring_meta, "views": {n: getattr(self, n) for n in names}}
+
+        best = snap()
+        tries, held = [best["gbs"]], []
+        ring_bytes = self.frame_window * self._ring.slot_stride
+        for k in range(self.PARTNER_TRIES):
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if free < self._arena_used + (k + 1) * self.PLACEMENT_SPACER + ring_bytes + (16 << 30):
+                break
+            held.append(self._arena_buf)
+            held.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
+            self._ring = self.frames = None  # the best ring stays referenced by `best`
+            try:
+                self._alloc()
+            except _abi.FFMPBackendError:
+                break
+            if self.ring != "seamless" or self._ring is None:
+                break
+            cur = snap()
+            tries.append(cur["gbs"])
+            if cur["gbs"] > best["gbs"]:
+                best = cur
+            cur = None
+            if best["gbs"] >= self.PAIR_FAST_GBS:
+                break
+        self._arena_buf, self._ring, self.ring = best["arena"], best["ring"], "seamless"
+        for n, v in best["views"].items():
+            setattr(self, n, v)
+        self.frames = self._ring.tensor
+        self._arena_used = self._arena_buf.numel()
+        torch.cuda.synchronize(self.device)
+        del held
+        self.potential.zero_()
+        self.frames[:self.frame_window].zero_()
+        self.ring_meta = dict(best["meta"], partner_tries=[round(g, 1) for g in tries])
+        best = None
+        torch.cuda.empty_cache()
+
+    def _adopt_ring_tensor(self) -> None:
+        self.frames = self._ring.tensor
+        self.potential.zero_()
+        self._build_structs()
+
     def _repair_slots(self) -> None:
+        """Rebuild slow slots and keep whichever ring cycles faster: a rebuild maps every slot at
+        new addresses and has left kept slots slower than before (round-1 repair logs), so the
+        old ring stays alive until the new one has been timed (SeamlessRing.rebuild keep_old)."""
         history = []
-        for _ in range(self.REPAIR_ROUNDS + 1):
-            ms = self._slot_ms()
+        ms = self._slot_ms()
+        for _ in range(self.REPAIR_ROUNDS):
             fast = min(ms.values())
             slow = [i for i, v in ms.items() if v > self.SLOW_SLOT * fast]
             history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)], "slow": slow})
-            if not slow or len(history) > self.REPAIR_ROUNDS:
+            if not slow:
                 break
-            self._ring.rebuild(sum(1 << i for i in slow), partner=self.potential)
-            self.frames = self._ring.tensor
-            self.potential.zero_()
-            self._build_structs()
+            # the tuning launches (and _clear_after_tuning's memsets) must be done before the
+            # rebuild's pairing probes write the potential plane on their own stream
+            torch.cuda.synchronize(self.device)
+            self._ring.rebuild(sum(1 << i for i in slow), partner=self.potential, keep_old=True)
+            self._adopt_ring_tensor()
+            new = self._slot_ms()
+            if sum(new.values()) < sum(ms.values()):
+                torch.cuda.synchronize(self.device)
+                self._ring.drop_previous()
+                ms = new
+            else:  # the rebuilt ring cycles slower: back to the previous one, stop repairing
+                history.append({"slot_ms": [round(new[i], 3) for i in sorted(new)], "reverted": True})
+                torch.cuda.synchronize(self.device)
+                self._ring.revert()
+                self._adopt_ring_tensor()
+                self._clear_after_tuning()
+                break
+        else:
+            history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)], "slow": []})
         self.ring_meta = dict(self._ring.info(), repair=history)
 
     def tuning(self) -> dict:
@@ -623,9 +704,19 @@ class FFMPVec:
             return (2 * G2, G2)
         return (G2, self.frames.stride(0))
 
+    # Seamless ring, wrap step (pair [W-1, W]): the newest frame goes to physical slot 0, which
+    # virtual slots 0 and W both map.  WRAP_VIA_ALIAS False: the raster writes it through slot
+    # 0's own addresses (negative frame stride from slot W-1); the state_m view still reads it
+    # through slot W.  Same bytes either way.
+    WRAP_VIA_ALIAS = True
+
     def _set_window(self, p: int) -> None:
         self._wpos = p
         self._obs_c.state_m = self.frames.data_ptr() + p * self.frames.stride(0) * self._fes
+        if self.ring == "seamless":
+            W, fs = self.frame_window, self.frames.stride(0)
+            wrap = p == W - 1 and not self.WRAP_VIA_ALIAS
+            self._obs_c.state_m_frame_stride = -(W - 1) * fs if wrap else fs
 
     def _raster_bytes(self, n: int, full: bool) -> int:
         """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs
@@ -636,6 +727,7 @@ class FFMPVec:
         return n * per
 
     def _raster_launch(self, full: bool, mask=None, timing: Optional[list] = None) -> None:
+        self._check_open()
         cpb, flags = self.raster_shape if full else self.raster_shape_newest
         flags |= 0 if full else _abi.RASTER_NEWEST
         if timing is not None:
@@ -666,6 +758,7 @@ class FFMPVec:
 
     def reset(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None, copy: bool = False):
         """Reset all envs (mask None: new episodes 0 from `seed`) or only masked ones."""
+        self._check_open()
         with torch.cuda.device(self.device):
             if seed is not None:
                 self.cfg = self.cfg.replace(seed=int(seed))
@@ -697,6 +790,7 @@ class FFMPVec:
 
     def step_state(self, actions: torch.Tensor) -> None:
         """Kernel 1 of a step: dynamics, lidar, reward/done, auto-reset, record."""
+        self._check_open()
         a = self._actions(actions)
         self._act_keepalive = a
         _abi.check(self.lib.ffmp_step_state(C.byref(self._cfg_c), self.num_envs, self.env_offset, a.data_ptr(),
@@ -705,6 +799,7 @@ class FFMPVec:
 
     def raster(self, mask: Optional[torch.Tensor] = None) -> None:
         """Re-raster the current observation (both frames, potential, flow) from the record."""
+        self._check_open()
         m = None if mask is None else mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
         self._raster_launch(True, m)
 
@@ -728,6 +823,7 @@ class FFMPVec:
 
     def _step_fused(self, actions, timing: Optional[list] = None) -> None:
         """Env step + raster in one launch (ffmp_step_fused): one block per env."""
+        self._check_open()
         a = self._actions(actions)
         self._act_keepalive = a
         full = self._next_window()
@@ -746,10 +842,12 @@ class FFMPVec:
     def raster_step(self, timing: Optional[list] = None) -> None:
         """Kernel 2 of a step (the HBM-bound hot kernel): slide the frame pair by one and raster
         the new frame + potential (+ flow), or both frames when the window wraps or W == 2."""
+        self._check_open()
         full = self._next_window()
         self._raster_launch(full, None, timing)
 
     def _step_pipelined(self, actions, timing) -> None:
+        self._check_open()
         a = self._actions(actions)
         self._act_keepalive = a
         main = torch.cuda.current_stream(self.device)
@@ -780,6 +878,7 @@ class FFMPVec:
 
         `timing`: optional list; (start, end, n_envs, algorithmic bytes, full) per raster launch
         (HIP events on the caller's stream) are appended to it."""
+        self._check_open()
         if self._needs_reset:
             raise RuntimeError("call reset() before step()")
         with torch.cuda.device(self.device):
@@ -860,14 +959,27 @@ class FFMPVec:
         return self.step(a, **kw)
 
     def close(self) -> None:
-        """Release the device buffers (the object is unusable afterwards)."""
+        """Release the device buffers (the object is unusable afterwards: every entry point that
+        would launch a kernel raises RuntimeError)."""
+        if self._closed:
+            return
+        self._closed = True
         self._needs_reset = True
         torch.cuda.synchronize(self.device)
         for name, _, _ in self._buffer_specs():
             setattr(self, name, None)
+        # the launch structs hold raw device pointers into the freed buffers
+        self._state_c = self._obs_c = self._out_c = None
+        self._slices = []
         self._arena_buf = None
         self._ring = None  # the seamless ring's pieces return to the process pool
         torch.cuda.empty_cache()
+
+    _closed = False
+
+    def _check_open(self) -> None:
+        if self._closed:
+            raise RuntimeError("FFMPVec is closed")
 
     # ------------------------------------------------------------ utilities
     def check_errors(self) -> None:
@@ -877,16 +989,34 @@ class FFMPVec:
             self.err.zero_()
             raise ValueError(f"invalid action id(s) passed to FFMPVec.step (error bits {v:#x})")
 
+    # simulator state, then the per-env observations and outputs the env kernel wrote (the planes
+    # are re-rastered from the record on load)
+    _SD_STATE = ("pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record")
+    _SD_OBS = ("state_g", "state_v", "state_t", "grad", "lidar", "reward", "done", "is_goal", "collision",
+               "truncated", "term_record", "term_obs")
+
     def state_dict(self) -> Dict[str, torch.Tensor]:
-        """Checkpoint of the simulator state (obs are re-derivable by raster())."""
-        return {"pose": self.pose.clone(), "goal": self.goal.clone(), "d0": self.d0.clone(),
-                "obst": self.obst.clone(), "obst_r": self.obst_r.clone(), "t": self.t.clone(),
-                "episode": self.episode.clone(), "record": self.record.clone(),
-                "seed": torch.tensor(self.cfg.seed, dtype=torch.int64), }
+        """Checkpoint: the simulator state plus the small observations and step outputs (the
+        planes are re-derived from the record by load_state_dict's raster())."""
+        self._check_open()
+        sd = {k: getattr(self, k).clone() for k in self._SD_STATE}
+        for k in self._SD_OBS:
+            v = getattr(self, k)
+            if v is not None:
+                sd[k] = v.clone()
+        sd["seed"] = torch.tensor(self.cfg.seed, dtype=torch.int64)
+        return sd
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
-        for k in ("pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record"):
+        """Restore a state_dict() of an env of the same config and num_envs (a fresh instance
+        included): every observation key of the saved env is reproduced."""
+        self._check_open()
+        for k in self._SD_STATE:
             getattr(self, k).copy_(sd[k])
+        for k in self._SD_OBS:
+            v = getattr(self, k)
+            if v is not None and k in sd:
+                v.copy_(sd[k])
         seed = int(sd["seed"])
         if seed != self.cfg.seed:
             self.cfg = self.cfg.replace(seed=seed)

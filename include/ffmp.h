@@ -147,7 +147,9 @@ typedef struct ffmp_obs {
   int64_t state_m_frame_stride; /* floats from env e's older frame to its newest; 0 = G*G.
                                    0/0 is the contiguous (N,2,G,G) layout.  A slot-major frame
                                    window (W, N, G, G) uses G*G / N*G*G with state_m at the
-                                   older slot (see FFMP_RASTER_NEWEST). */
+                                   older slot (see FFMP_RASTER_NEWEST).  May be negative (the
+                                   newest frame in a lower slot: a seamless ring's wrap step can
+                                   write slot 0 through its first mapping instead of slot W's). */
   int32_t format;   /* FFMP_OBS_F32 (0) or FFMP_OBS_U8F16 */
   int32_t reserved;
 } ffmp_obs_t;
@@ -347,8 +349,12 @@ int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const vo
                      int64_t partner_bytes, ffmp_ring_t** ring, void** base, int64_t* slot_stride);
 /* A new ring (new addresses) with the pieces of `old`'s slots in replace_mask (bit i = slot i)
  * replaced by other pieces (chosen as in ffmp_ring_create, never the replaced ones), the other
- * slots' pieces moved over.  For a caller whose timing shows a slot pairing badly; `old` must
- * not be used for data afterwards (its addresses still alias the moved pieces) — drop it. */
+ * slots' pieces shared with `old`.  For a caller whose timing shows a slot pairing badly.
+ * `old` stays valid: the caller can time both rings and destroy the slower one (the kept
+ * slots are the same memory in both, so only one of them should be written from then on).
+ * A piece returns to the pool when the last ring holding it is gone; the pool is drawn from
+ * only after a device synchronize (ffmp_ring_create / rebuild), so GPU work still writing a
+ * dropped ring never overlaps the piece's next use. */
 int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partner, int64_t partner_bytes,
                       ffmp_ring_t** ring, void** base, int64_t* slot_stride);
 int ffmp_ring_destroy(ffmp_ring_t* ring);

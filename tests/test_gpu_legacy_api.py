@@ -218,3 +218,47 @@ def test_vector_env_surface():
     b.close()
     with pytest.raises(RuntimeError):
         b.step(act)
+
+
+@pytest.mark.parametrize("window", [2, 4])
+def test_checkpoint_into_a_fresh_env_restores_every_obs(window):
+    """load_state_dict into a NEW instance reproduces every observation key and step output of
+    the saved env (not only the planes), and both continue identically."""
+    cfg = FFMPConfig(grid=64, n_obst=8, n_beams=32, moving=True, max_steps=5, seed=23)
+    a = P.FFMPVec(9, cfg, device="cuda:0", keep_terminal=True, frame_window=window)
+    a.reset()
+    g = torch.Generator().manual_seed(4)
+    for _ in range(7):  # through truncations (max_steps 5) so term_* and done are populated
+        a.step(torch.randint(0, 28, (9,), generator=g).to("cuda:0"))
+    sd = a.state_dict()
+    b = P.FFMPVec(9, cfg, device="cuda:0", keep_terminal=True, frame_window=window)
+    b.load_state_dict(sd)
+    oa, ob = a.obs, b.obs
+    assert set(oa) == set(ob)
+    for k in oa:
+        assert torch.equal(oa[k], ob[k]), k
+    for k in ("reward", "done", "is_goal", "collision", "truncated", "term_record", "term_obs", "t", "episode"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert bool(a.state_g.abs().sum() > 0) and bool(a.lidar.isfinite().any())
+    for _ in range(6):
+        act = torch.randint(0, 28, (9,), generator=g).to("cuda:0")
+        ra, rb = a.step(act), b.step(act)
+        for k in ra[0]:
+            assert torch.equal(ra[0][k], rb[0][k]), k
+        assert torch.equal(ra[1], rb[1]) and torch.equal(ra[2], rb[2])
+
+
+def test_closed_env_refuses_every_launch():
+    """After close() no entry point launches a kernel on the freed buffers."""
+    cfg = FFMPConfig(grid=64, n_obst=4, n_beams=16, moving=True, seed=3)
+    v = P.FFMPVec(4, cfg, device="cuda:0", frame_window=3)
+    v.reset()
+    sd = v.state_dict()
+    act = torch.zeros(4, dtype=torch.int64, device="cuda:0")
+    v.close()
+    v.close()  # idempotent
+    for call in (lambda: v.reset(), lambda: v.reset(mask=torch.ones(4, dtype=torch.bool)),
+                 lambda: v.step(act), lambda: v.step_state(act), lambda: v.raster(), lambda: v.raster_step(),
+                 lambda: v._step_fused(act), lambda: v.load_state_dict(sd), lambda: v.state_dict()):
+        with pytest.raises(RuntimeError, match="closed"):
+            call()

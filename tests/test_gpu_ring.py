@@ -96,3 +96,61 @@ def test_slot_written_matches_the_step(fused):
         torch.cuda.synchronize()
         whole = [i for i in range(W) if bool((env.frames[i] != -3.0).all())]
         assert whole == [env._slot_written(k)], (k, whole)
+
+
+def test_rebuild_keep_old_then_revert_or_keep():
+    """rebuild(keep_old=True) leaves the old ring whole (its replaced slots keep their bytes);
+    revert() makes it current again and drop_previous() releases it; pieces of the released
+    ring reach the pool."""
+    lib = _abi.load()
+    ring = _abi.SeamlessRing(DEV, (3, 40, 40), 4)
+    _fill(ring.tensor, 4)
+    old_t = ring.tensor
+    ring.rebuild(0b0010, keep_old=True)  # replace slot 1
+    new_t = ring.tensor
+    assert new_t.data_ptr() != old_t.data_ptr()
+    assert float(new_t[2].min()) == 3.0 and float(new_t[0].max()) == 1.0  # kept slots shared
+    new_t[1].fill_(-5.0)
+    torch.cuda.synchronize()
+    assert float(old_t[1].min()) == 2.0 and float(old_t[1].max()) == 2.0  # old slot 1 untouched
+    new_t[2].fill_(8.0)  # a kept slot is the same memory in both rings
+    torch.cuda.synchronize()
+    assert float(old_t[2].min()) == 8.0
+    pooled = lib.ffmp_ring_pool_bytes(DEV)
+    ring.revert()
+    assert ring.tensor.data_ptr() == old_t.data_ptr() and ring.info()["reverts"] == 1
+    del new_t
+    gc.collect()
+    assert lib.ffmp_ring_pool_bytes(DEV) == pooled + ring.slot_stride  # the new slot-1 piece
+    ring.rebuild(0b0001, keep_old=True)
+    ring.drop_previous()
+    del old_t
+    gc.collect()
+    assert lib.ffmp_ring_pool_bytes(DEV) >= pooled + ring.slot_stride  # old slot 0 freed (new one drawn)
+    t = ring.tensor
+    t[0].fill_(4.0)
+    torch.cuda.synchronize()
+    assert torch.equal(t[4], t[0]) and float(t[1].max()) == 2.0
+    with pytest.raises(RuntimeError):
+        ring.revert()
+
+
+def test_repair_keeps_a_working_ring():
+    """_repair_slots with every slot declared slow rebuilds, times, and keeps or reverts; either
+    way the env still matches the contiguous layout bit for bit."""
+    from flow_field_based_motion_planner_amd.config import FFMPConfig
+    from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+    cfg = FFMPConfig(grid=64, n_obst=6, n_beams=16, moving=True, max_steps=6, seed=9)
+    a = FFMPVec(12, cfg, device="cuda:0", frame_window=2)
+    b = FFMPVec(12, cfg, device="cuda:0", frame_window=4, seamless=True, autotune=False)
+    b.SLOW_SLOT = -1.0  # every slot is "slow": forces the rebuild + keep/revert path
+    b._repair_slots()
+    hist = b.ring_meta["repair"]
+    assert b._ring.info()["rebuilds"] >= 1 and len(hist) >= 2
+    a.reset()
+    b.reset()
+    g = torch.Generator().manual_seed(1)
+    for _ in range(10):
+        act = torch.randint(0, 28, (12,), generator=g).to("cuda:0")
+        oa, ob = a.step(act)[0], b.step(act)[0]
+        assert torch.equal(oa["state_m"], ob["state_m"]) and torch.equal(oa["potential"], ob["potential"])

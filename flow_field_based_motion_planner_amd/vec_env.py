@@ -505,7 +505,7 @@ class FFMPVec:
                 break
         else:
             history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)], "slow": []})
-        self.ring_meta = dict(self._ring.info(), repair=history)
+        self.ring_meta = dict(self.ring_meta or {}, **self._ring.info(), repair=history)
 
     def tuning(self) -> dict:
         """The launch choices of this instance (pass as FFMPVec(tuning=...) to skip the autotune)."""

@@ -591,12 +591,16 @@ class FFMPVec:
     # The compact format (obs_format="u8f16") writes 3 bytes per cell and is bound by the per-task
     # cull / wall / index work rather than by HBM (tools/compact_probe.py): 16 cells per lane
     # (1024-cell wave tasks) by default, tiles R x 1024/R; NARROW = the 4-cells-per-lane kernel.
+    # (round 2: the 16-cells-per-lane tiles hoist their columns' work out of the tile loop;
+    # tools/compact_shapes.py: whole-plane blocks, 4- or 16-cell lanes, 1.46-1.55 ms at C3)
     COMPACT_SHAPES = (
-        (16384, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW), (16384, _abi.RASTER_NT | _abi.RASTER_TILE16),
-        (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (16384, _abi.RASTER_NT | _abi.RASTER_TILE4),
-        (8192, _abi.RASTER_NT | _abi.RASTER_TILE16), (32768, _abi.RASTER_NT | _abi.RASTER_TILE16),
-        (16384, _abi.RASTER_PLAIN | _abi.RASTER_TILE16), (16384, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE16),
-        (16384, _abi.RASTER_NT), (8192, _abi.RASTER_NT | _abi.RASTER_TILE8),
+        (65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW),
+        (32768, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW),
+        (16384, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW),
+        (65536, _abi.RASTER_PLAIN | _abi.RASTER_TILE16), (32768, _abi.RASTER_NT | _abi.RASTER_TILE16),
+        (16384, _abi.RASTER_NT | _abi.RASTER_TILE16), (65536, _abi.RASTER_NT | _abi.RASTER_TILE4),
+        (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (16384, _abi.RASTER_PLAIN | _abi.RASTER_TILE16),
+        (32768, _abi.RASTER_PLAIN | _abi.RASTER_TILE4 | _abi.RASTER_NARROW),
     )
     COMPACT_FUSED_FLAGS = (
         _abi.RASTER_NT | _abi.RASTER_TILE16, _abi.RASTER_NT | _abi.RASTER_TILE8, _abi.RASTER_NT | _abi.RASTER_TILE4,

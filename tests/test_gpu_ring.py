@@ -168,6 +168,7 @@ def test_partner_relocation_keeps_a_consistent_env():
 
     class Picky(FFMPVec):
         PAIR_FAST_GBS = 1e9  # nothing is fast enough: every try runs
+        REPAIR_ROUNDS = 0    # (a slot rebuild would report only its new pieces' probes)
 
     cfg = FFMPConfig(grid=256, n_obst=8, n_beams=32, moving=True, max_steps=5, seed=17)
     n = 8192  # 2 GiB frame slots (1 GiB pieces, probed) + 2 GiB potential plane

@@ -1,0 +1,44 @@
+"""Compact-format (uint8 frames, float16 potential) newest-only raster at C3 for a list of launch
+shapes, on ONE instance (no autotune): mean raster ms per launch over 2 x 8 steps of the real step
+loop (HIP events around each raster launch).  Usage: python tools/compact_shapes.py [cfg] [f32|u8f16]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from flow_field_based_motion_planner_amd import _abi  # noqa: E402
+from flow_field_based_motion_planner_amd.config import PRESETS  # noqa: E402
+from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
+
+NT, PL, XCD = _abi.RASTER_NT, _abi.RASTER_PLAIN, _abi.RASTER_XCD
+T4, T8, T16, NAR = _abi.RASTER_TILE4, _abi.RASTER_TILE8, _abi.RASTER_TILE16, _abi.RASTER_NARROW
+SHAPES = [(16384, NT | T4 | NAR), (32768, NT | T16), (65536, NT | T16), (65536, PL | T16), (32768, PL | T16),
+          (65536, NT | XCD | T16), (65536, NT | T8), (65536, NT | T4), (32768, NT | T4 | NAR), (65536, NT | T4 | NAR)]
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "C3"
+    fmt = sys.argv[2] if len(sys.argv) > 2 else "u8f16"
+    pr = PRESETS[name]
+    n = pr["n_envs"] // max(1, pr["gpus"])
+    env = FFMPVec(n, name, device="cuda:0", obs_format=fmt, autotune=False, fused=False)
+    a = torch.full((n,), 10, dtype=torch.int64, device="cuda:0")
+    for rep in range(2):
+        for shape in SHAPES:
+            env.raster_shape = env.raster_shape_newest = shape
+            env.reset()
+            for _ in range(2):
+                env.step(a)
+            t = []
+            for _ in range(8):
+                env.step(a, timing=t)
+            torch.cuda.synchronize()
+            ms = [r[0].elapsed_time(r[1]) for r in t]
+            b = sum(r[3] for r in t)
+            print(f"rep {rep} shape {shape[0]:6d}/{shape[1]:4d}: raster {sum(ms) / len(ms):.3f} ms "
+                  f"{b / (sum(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -673,131 +673,136 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
     const int ntiles = ((qend - qbeg) / G / R) * ncb;
     const int r = lane / lanes_per_row;
     const int cl = (lane - r * lanes_per_row) * CPL;
-    if ((4 % ncb) == 0) {
-      // The wave's column band never changes (tile t has band t / ncb and column band
-      // t % ncb = wave % ncb; G = 256 with any TILE flag): this lane's CPL columns, their ego y
-      // and (y - goal y)^2 are computed once for the block instead of per tile, the attractive
+    if ((4 % ncb) == 0 || (ncb % 4) == 0) {
+      // Column-band-major tiles: wave w takes column bands w, w + 4, ... (ncb >= 4) or the
+      // bands b = w / ncb, + 4 / ncb, ... of column band w % ncb (ncb | 4), so per column band
+      // this lane's CPL columns, their ego y and (y - goal y)^2 are computed once instead of per
+      // tile (the 4 waves still write neighbouring columns of the same rows at once), the attractive
       // term is then one add + one multiply per cell (packed pairs), and the occupancy is kept as
       // the stored bytes (0x00 / 0xFF; float32: v_cvt_f32_ubyte gives 0 / 255) instead of floats.
       // The same float32 operations in the same order as `task`: bit-identical planes.  (Round 2:
       // the compact raster's VALU instructions per launch 1.02e9 -> 0.42e9, profiles/r02_compact.txt.)
       typedef float f2 __attribute__((ext_vector_type(2)));
       constexpr int NP = CPL / 2, NW = CPL / 4;
-      const int jb = (wave % ncb) * C, j = jb + cl;
-      const float by0 = (float)jb * res - half, by1 = (float)(jb + C - 1) * res - half;
-      f2 ey2[NP], dyy2[NP];
-#pragma unroll
-      for (int p2 = 0; p2 < NP; ++p2) {
-        ey2[p2] = f2{(float)(j + 2 * p2) * res - half, (float)(j + 2 * p2 + 1) * res - half};
-        const f2 dy = ey2[p2] - gy;
-        dyy2[p2] = dy * dy;
-      }
+      const int nbands = ntiles / ncb;
+      const int wpc = ncb < 4 ? 4 / ncb : 1;  // waves per column band
       const f2 hka = {cfg.half_ka_f, cfg.half_ka_f};
-      for (int t = wave; t < ntiles; t += 4) {
-        const int i0 = row0 + (t / ncb) * R;
-        const int i = i0 + r;
-        const int q = i * G + j;
-        const float bx0 = (float)i0 * res - half, bx1 = (float)(i0 + R - 1) * res - half;
-        const uint64_t mc = __ballot(has && box_dist2(oc.x, oc.y, bx0, bx1, by0, by1) <= rc2);
-        const uint64_t mp = write_old ? __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2) : 0ull;
-        const uint64_t wb = __ballot(lane >= 8 || corner_inside(cfg, hq, (lane & 1) ? bx1 : bx0,
-                                                                 (lane & 2) ? by1 : by0));
-        const bool walls_c = (wb & 0xFull) != 0xFull;
-        const bool walls_p = write_old && (wb & 0xF0ull) != 0xF0ull;
-        const float ex = (float)i * res - half;
-        uint32_t wc[NW], wp[NW];
+      for (int cb = wave % ncb; cb < ncb; cb += 4) {
+        const int jb = cb * C, j = jb + cl;
+        const float by0 = (float)jb * res - half, by1 = (float)(jb + C - 1) * res - half;
+        f2 ey2[NP], dyy2[NP];
 #pragma unroll
-        for (int w = 0; w < NW; ++w) wc[w] = wp[w] = 0u;
-        f2 U2[NP];
-        if (with_pot) {
-          const float dx = ex - gx;
-          const f2 dxx = {dx * dx, dx * dx};
-#pragma unroll
-          for (int p2 = 0; p2 < NP; ++p2) U2[p2] = hka * (dxx + dyy2[p2]);
+        for (int p2 = 0; p2 < NP; ++p2) {
+          ey2[p2] = f2{(float)(j + 2 * p2) * res - half, (float)(j + 2 * p2 + 1) * res - half};
+          const f2 dy = ey2[p2] - gy;
+          dyy2[p2] = dy * dy;
         }
-        if (walls_c) {
+        for (int band = wave / ncb; band < nbands; band += wpc) {
+          const int i0 = row0 + band * R;
+          const int i = i0 + r;
+          const int q = i * G + j;
+          const float bx0 = (float)i0 * res - half, bx1 = (float)(i0 + R - 1) * res - half;
+          const uint64_t mc = __ballot(has && box_dist2(oc.x, oc.y, bx0, bx1, by0, by1) <= rc2);
+          const uint64_t mp = write_old ? __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2) : 0ull;
+          const uint64_t wb = __ballot(lane >= 8 || corner_inside(cfg, hq, (lane & 1) ? bx1 : bx0,
+                                                                   (lane & 2) ? by1 : by0));
+          const bool walls_c = (wb & 0xFull) != 0xFull;
+          const bool walls_p = write_old && (wb & 0xF0ull) != 0xF0ull;
+          const float ex = (float)i * res - half;
+          uint32_t wc[NW], wp[NW];
 #pragma unroll
-          for (int u = 0; u < CPL; ++u)
-            if (outside_world(cfg, hc, ex, ey2[u >> 1][u & 1])) wc[u >> 2] |= 0xFFu << (8 * (u & 3));
-        }
-        if (walls_p) {
+          for (int w = 0; w < NW; ++w) wc[w] = wp[w] = 0u;
+          f2 U2[NP];
+          if (with_pot) {
+            const float dx = ex - gx;
+            const f2 dxx = {dx * dx, dx * dx};
 #pragma unroll
-          for (int u = 0; u < CPL; ++u)
-            if (outside_world(cfg, hp, ex, ey2[u >> 1][u & 1])) wp[u >> 2] |= 0xFFu << (8 * (u & 3));
-        }
-        for (uint64_t m = mp; m; m &= m - 1) {
-          const float4 o = s_prev[__builtin_ctzll(m)];
-#pragma unroll
-          for (int u = 0; u < CPL; ++u)
-            if (in_disc(ex, ey2[u >> 1][u & 1], o)) wp[u >> 2] |= 0xFFu << (8 * (u & 3));
-        }
-        float fx[FLOW ? CPL : 1], fy[FLOW ? CPL : 1];
-        uint32_t fset = 0u;  // FLOW: cells already covered by a lower-index disc
-        if (FLOW) {
-#pragma unroll
-          for (int u = 0; u < CPL; ++u) fx[u] = fy[u] = 0.0f;
-        }
-        for (uint64_t m = mc; m; m &= m - 1) {
-          const int k = __builtin_ctzll(m);
-          const float4 o = s_cur[k];
-          const float reach2 = rep_reach2(cfg, o.w);
-          const float dx = ex - o.x;
-          const f2 dxx = {dx * dx, dx * dx};
-#pragma unroll
-          for (int p2 = 0; p2 < NP; ++p2) {
-            const f2 dy = ey2[p2] - o.y;
-            const f2 d2 = dxx + dy * dy;  // in_disc's and add_repulsive's operand
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              const int u = 2 * p2 + c;
-              const bool d = d2[c] <= o.z;
-              if (d) wc[u >> 2] |= 0xFFu << (8 * (u & 3));
-              if (FLOW && d && !((fset >> u) & 1u)) {
-                fx[u] = s_vel[k].x;
-                fy[u] = s_vel[k].y;
-                fset |= 1u << u;
-              }
-              if (with_pot) U2[p2][c] = add_repulsive_s(cfg, U2[p2][c], d2[c], o.w, reach2);
-            }
+            for (int p2 = 0; p2 < NP; ++p2) U2[p2] = hka * (dxx + dyy2[p2]);
           }
-        }
-        if (FMT == FMT_CT16) {
-          if (write_old) store16_w<NT>(b0 + q, wp);
-          store16_w<NT>(b1 + q, wc);
-          if (hp16) {
-            const f16x8 lo = {(_Float16)U2[0].x, (_Float16)U2[0].y, (_Float16)U2[1].x, (_Float16)U2[1].y,
-                              (_Float16)U2[2].x, (_Float16)U2[2].y, (_Float16)U2[3].x, (_Float16)U2[3].y};
-            const f16x8 hi = {(_Float16)U2[NP - 4].x, (_Float16)U2[NP - 4].y, (_Float16)U2[NP - 3].x,
-                              (_Float16)U2[NP - 3].y, (_Float16)U2[NP - 2].x, (_Float16)U2[NP - 2].y,
-                              (_Float16)U2[NP - 1].x, (_Float16)U2[NP - 1].y};
-            if (NT) {
-              __builtin_nontemporal_store(lo, reinterpret_cast<f16x8*>(hp16 + q));
-              __builtin_nontemporal_store(hi, reinterpret_cast<f16x8*>(hp16 + q + 8));
-            } else {
-              *reinterpret_cast<f16x8*>(hp16 + q) = lo;
-              *reinterpret_cast<f16x8*>(hp16 + q + 8) = hi;
-            }
+          if (walls_c) {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+              if (outside_world(cfg, hc, ex, ey2[u >> 1][u & 1])) wc[u >> 2] |= 0xFFu << (8 * (u & 3));
           }
-        } else if (FMT == FMT_CT4) {
-          if (NT) {
-            if (write_old) __builtin_nontemporal_store(wp[0], reinterpret_cast<uint32_t*>(b0 + q));
-            __builtin_nontemporal_store(wc[0], reinterpret_cast<uint32_t*>(b1 + q));
-          } else {
-            if (write_old) *reinterpret_cast<uint32_t*>(b0 + q) = wp[0];
-            *reinterpret_cast<uint32_t*>(b1 + q) = wc[0];
+          if (walls_p) {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+              if (outside_world(cfg, hp, ex, ey2[u >> 1][u & 1])) wp[u >> 2] |= 0xFFu << (8 * (u & 3));
           }
-          if (hp16) store4_h<NT>(hp16 + q, U2[0].x, U2[0].y, U2[NP - 1].x, U2[NP - 1].y);
-        } else {
-          // byte 0xFF -> 255.0f, 0 -> 0.0f: the reference layout's occ * 255 values
-          if (write_old)
-            store4<NT>(m0 + q, (float)(wp[0] & 0xFFu), (float)((wp[0] >> 8) & 0xFFu), (float)((wp[0] >> 16) & 0xFFu),
-                       (float)(wp[0] >> 24));
-          store4<NT>(m1 + q, (float)(wc[0] & 0xFFu), (float)((wc[0] >> 8) & 0xFFu), (float)((wc[0] >> 16) & 0xFFu),
-                     (float)(wc[0] >> 24));
-          if (pp) store4<NT>(pp + q, U2[0].x, U2[0].y, U2[NP - 1].x, U2[NP - 1].y);
+          for (uint64_t m = mp; m; m &= m - 1) {
+            const float4 o = s_prev[__builtin_ctzll(m)];
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+              if (in_disc(ex, ey2[u >> 1][u & 1], o)) wp[u >> 2] |= 0xFFu << (8 * (u & 3));
+          }
+          float fx[FLOW ? CPL : 1], fy[FLOW ? CPL : 1];
+          uint32_t fset = 0u;  // FLOW: cells already covered by a lower-index disc
           if (FLOW) {
-            store4<NT>(f0 + q, fx[0], fx[1 % CPL], fx[2 % CPL], fx[3 % CPL]);
-            store4<NT>(f0 + G2 + q, fy[0], fy[1 % CPL], fy[2 % CPL], fy[3 % CPL]);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) fx[u] = fy[u] = 0.0f;
+          }
+          for (uint64_t m = mc; m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            const float4 o = s_cur[k];
+            const float reach2 = rep_reach2(cfg, o.w);
+            const float dx = ex - o.x;
+            const f2 dxx = {dx * dx, dx * dx};
+#pragma unroll
+            for (int p2 = 0; p2 < NP; ++p2) {
+              const f2 dy = ey2[p2] - o.y;
+              const f2 d2 = dxx + dy * dy;  // in_disc's and add_repulsive's operand
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                const int u = 2 * p2 + c;
+                const bool d = d2[c] <= o.z;
+                if (d) wc[u >> 2] |= 0xFFu << (8 * (u & 3));
+                if (FLOW && d && !((fset >> u) & 1u)) {
+                  fx[u] = s_vel[k].x;
+                  fy[u] = s_vel[k].y;
+                  fset |= 1u << u;
+                }
+                if (with_pot) U2[p2][c] = add_repulsive_s(cfg, U2[p2][c], d2[c], o.w, reach2);
+              }
+            }
+          }
+          if (FMT == FMT_CT16) {
+            if (write_old) store16_w<NT>(b0 + q, wp);
+            store16_w<NT>(b1 + q, wc);
+            if (hp16) {
+              const f16x8 lo = {(_Float16)U2[0].x, (_Float16)U2[0].y, (_Float16)U2[1].x, (_Float16)U2[1].y,
+                                (_Float16)U2[2].x, (_Float16)U2[2].y, (_Float16)U2[3].x, (_Float16)U2[3].y};
+              const f16x8 hi = {(_Float16)U2[NP - 4].x, (_Float16)U2[NP - 4].y, (_Float16)U2[NP - 3].x,
+                                (_Float16)U2[NP - 3].y, (_Float16)U2[NP - 2].x, (_Float16)U2[NP - 2].y,
+                                (_Float16)U2[NP - 1].x, (_Float16)U2[NP - 1].y};
+              if (NT) {
+                __builtin_nontemporal_store(lo, reinterpret_cast<f16x8*>(hp16 + q));
+                __builtin_nontemporal_store(hi, reinterpret_cast<f16x8*>(hp16 + q + 8));
+              } else {
+                *reinterpret_cast<f16x8*>(hp16 + q) = lo;
+                *reinterpret_cast<f16x8*>(hp16 + q + 8) = hi;
+              }
+            }
+          } else if (FMT == FMT_CT4) {
+            if (NT) {
+              if (write_old) __builtin_nontemporal_store(wp[0], reinterpret_cast<uint32_t*>(b0 + q));
+              __builtin_nontemporal_store(wc[0], reinterpret_cast<uint32_t*>(b1 + q));
+            } else {
+              if (write_old) *reinterpret_cast<uint32_t*>(b0 + q) = wp[0];
+              *reinterpret_cast<uint32_t*>(b1 + q) = wc[0];
+            }
+            if (hp16) store4_h<NT>(hp16 + q, U2[0].x, U2[0].y, U2[NP - 1].x, U2[NP - 1].y);
+          } else {
+            // byte 0xFF -> 255.0f, 0 -> 0.0f: the reference layout's occ * 255 values
+            if (write_old)
+              store4<NT>(m0 + q, (float)(wp[0] & 0xFFu), (float)((wp[0] >> 8) & 0xFFu), (float)((wp[0] >> 16) & 0xFFu),
+                         (float)(wp[0] >> 24));
+            store4<NT>(m1 + q, (float)(wc[0] & 0xFFu), (float)((wc[0] >> 8) & 0xFFu), (float)((wc[0] >> 16) & 0xFFu),
+                       (float)(wc[0] >> 24));
+            if (pp) store4<NT>(pp + q, U2[0].x, U2[0].y, U2[NP - 1].x, U2[NP - 1].y);
+            if (FLOW) {
+              store4<NT>(f0 + q, fx[0], fx[1 % CPL], fx[2 % CPL], fx[3 % CPL]);
+              store4<NT>(f0 + G2 + q, fy[0], fy[1 % CPL], fy[2 % CPL], fy[3 % CPL]);
+            }
           }
         }
       }

@@ -163,7 +163,7 @@ def test_raster_split_over_launches():
                               pot[j].astype(np.float16).view(np.uint16)), int(e)
 
 
-@pytest.mark.parametrize("grid", [256, 64, 96, 100])
+@pytest.mark.parametrize("grid", [256, 64, 96, 100, 512, 192])
 def test_compact_shapes_identical(grid):
     """Every compact launch shape (16 or 4 cells per lane, 1-D chunks or R x C tiles, fused or
     two-launch, full and newest-only launches) writes the float32 layout's planes, converted, bit

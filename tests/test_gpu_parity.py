@@ -278,7 +278,7 @@ def test_raster_shapes_identical():
         assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), shape
 
 
-@pytest.mark.parametrize("grid", [256, 96, 100])
+@pytest.mark.parametrize("grid", [256, 96, 100, 512, 192])
 def test_tile_shapes_identical_with_flow(grid):
     """2-D wave tiles (R = 2, 4, 8) write the same frames, potential and flow planes as the
     256-cell chunks, in full and newest-only launches (G = 96: only R = 8 tiles apply; G = 100:

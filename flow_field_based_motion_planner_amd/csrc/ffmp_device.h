@@ -242,12 +242,18 @@ FFMP_DEV float attractive(const ffmp_cfg_t& cfg, float ex, float ey, float gx, f
   return cfg.half_ka_f * (dx * dx + dy * dy);
 }
 
-// Full (unculled) potential at cell (i, j) — used for the gradient lookup.
+// Potential at cell (i, j) over all K discs — used for the gradient lookup.  The raster's
+// arithmetic (add_repulsive_s: the same float32 operations as add_repulsive, skipping discs out
+// of repulsive reach), so the gradient is the central difference of the raster's plane.
 FFMP_DEV float potential_cell(const ffmp_cfg_t& cfg, const float4* obs, int K, float gx, float gy,
                               int i, int j) {
   const float ex = cell_coord(cfg, i), ey = cell_coord(cfg, j);
   float U = attractive(cfg, ex, ey, gx, gy);
-  for (int k = 0; k < K; ++k) U = add_repulsive(cfg, U, ex, ey, obs[k]);
+  for (int k = 0; k < K; ++k) {
+    const float4 o = obs[k];
+    const float dx = ex - o.x, dy = ey - o.y;
+    U = add_repulsive_s(cfg, U, dx * dx + dy * dy, o.w, rep_reach2(cfg, o.w));
+  }
   return U;
 }
 
@@ -302,10 +308,31 @@ FFMP_DEV LidarScene lidar_scene(const ffmp_cfg_t& cfg, double x, double y, doubl
   return sc;
 }
 
+// Per-disc lidar operands, written by disc k's lane before the beams (LDS): the disc centre
+// relative to the sensor (rx, ry), |rel|^2 and r^2 — the same float64 operations lidar_beam
+// did per beam, done once per disc.
+FFMP_DEV void lidar_disc(double x, double y, double ox, double oy, double r, double* rxa, double* rya, double* rra,
+                         double* r2a, int k) {
+  const double rx = ox - x, ry = oy - y;
+  rxa[k] = rx;
+  rya[k] = ry;
+  rra[k] = rx * rx + ry * ry;
+  r2a[k] = r * r;
+}
+
+// False only if the wall hit h = num / den (num, den of one sign) is certainly beyond L, so the
+// float64 division can be skipped without changing any range: |num| > (L*|den|)(1 + 2^-40) in
+// float64 means the exact quotient exceeds L(1 + 2^-41), and its rounding stays above L.
+FFMP_DEV bool wall_in_reach(double num, double den, double L) {
+  return !(fabs(num) > (L * fabs(den)) * (1.0 + 0x1p-40));
+}
+
 // One lidar beam (float64): nearest of the scene's discs and walls.  Returns +inf for no
-// return within lidar_max, -inf if the origin is inside a disc.
+// return within lidar_max, -inf if the origin is inside a disc.  rxa / rya / rra / r2a: the
+// scene's discs as lidar_disc wrote them.
 FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x, double y, double c, double s,
-                           double bc, double bs, const double* ox, const double* oy, const double* orad) {
+                           double bc, double bs, const double* rxa, const double* rya, const double* rra,
+                           const double* r2a) {
   const double inf = __builtin_inf();
   if (sc.inside) return -inf;
   const double dirx = c * bc - s * bs;
@@ -313,9 +340,9 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x
   double best = inf;
   for (uint64_t m = sc.mask; m; m &= m - 1) {
     const int k = __builtin_ctzll(m);
-    const double rx = ox[k] - x, ry = oy[k] - y;
-    const double rr = rx * rx + ry * ry;
-    const double r2 = orad[k] * orad[k];
+    const double rx = rxa[k], ry = rya[k];
+    const double rr = rra[k];
+    const double r2 = r2a[k];
     const double tp = rx * dirx + ry * diry;
     if (tp > 0.0) {
       const double perp = rr - tp * tp;
@@ -325,11 +352,11 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x
       }
     }
   }
-  const double W = cfg.world_half;
-  if (dirx > 0.0) { if (sc.wxp) { const double h = (W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; } }
-  else if (dirx < 0.0) { if (sc.wxn) { const double h = (-W - x) / dirx; if (h <= cfg.lidar_max && h < best) best = h; } }
-  if (diry > 0.0) { if (sc.wyp) { const double h = (W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; } }
-  else if (diry < 0.0) { if (sc.wyn) { const double h = (-W - y) / diry; if (h <= cfg.lidar_max && h < best) best = h; } }
+  const double W = cfg.world_half, L = cfg.lidar_max;
+  if (dirx > 0.0) { if (sc.wxp && wall_in_reach(W - x, dirx, L)) { const double h = (W - x) / dirx; if (h <= L && h < best) best = h; } }
+  else if (dirx < 0.0) { if (sc.wxn && wall_in_reach(-W - x, dirx, L)) { const double h = (-W - x) / dirx; if (h <= L && h < best) best = h; } }
+  if (diry > 0.0) { if (sc.wyp && wall_in_reach(W - y, diry, L)) { const double h = (W - y) / diry; if (h <= L && h < best) best = h; } }
+  else if (diry < 0.0) { if (sc.wyn && wall_in_reach(-W - y, diry, L)) { const double h = (-W - y) / diry; if (h <= L && h < best) best = h; } }
   return best;
 }
 

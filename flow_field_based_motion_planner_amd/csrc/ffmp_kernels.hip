@@ -170,7 +170,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
                                                        const int64_t* __restrict__ action, int32_t initial,
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
                                                        const ffmp_out_t& out, int64_t e, int lane, double* s_ox,
-                                                       double* s_oy, double* s_or, float4* s_ecur,
+                                                       double* s_oy, double* s_or, double* s_orr, float4* s_ecur,
                                                        float4* s_eprev) {
   static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
   const int K = cfg.n_obst;
@@ -228,7 +228,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     t_obs = (float)cfg.dt;
   }
 
-  if (has_obst) { s_ox[lane] = my.x; s_oy[lane] = my.y; s_or[lane] = my.r; }
+  if (has_obst) lidar_disc(x1, y1, my.x, my.y, my.r, s_ox, s_oy, s_orr, s_or, lane);
   double c1 = cos(yaw1), s1 = sin(yaw1);
   if (has_obst) s_ecur[lane] = ego_obst(my, x1, y1, c1, s1);
   wave_sync();
@@ -251,7 +251,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
     for (int l = lane; l < L; l += LPE) {
       const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_or);
+                                  s_ox, s_oy, s_orr, s_or);
       const float rf = (float)r;
       ob.lidar[e * L + l] = rf;
       c_lidar |= beam_collides(rf, cfg.robot_r);
@@ -291,7 +291,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     if (has_obst) my = sample_obstacle(cfg, genv, episode, lane, ep);
     c1 = cos(yaw1); s1 = sin(yaw1);
     if (has_obst) {
-      s_ox[lane] = my.x; s_oy[lane] = my.y; s_or[lane] = my.r;
+      lidar_disc(x1, y1, my.x, my.y, my.r, s_ox, s_oy, s_orr, s_or, lane);
       const float4 eo = ego_obst(my, x1, y1, c1, s1);
       s_ecur[lane] = eo;
       s_eprev[lane] = eo;  // temporal stack duplicated on the first step (train.py:475-478)
@@ -312,7 +312,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
     for (int l = lane; l < L; l += LPE) {
       const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_or);
+                                  s_ox, s_oy, s_orr, s_or);
       ob.lidar[e * L + l] = (float)r;
     }
   }
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
                                                  ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
   constexpr int EPW = 64 / LPE;  // envs per wave
   __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
-      s_ora[kEnvWaves][FFMP_MAX_OBST];
+      s_ora[kEnvWaves][FFMP_MAX_OBST], s_orra[kEnvWaves][FFMP_MAX_OBST];
   __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
 
   const int wv = threadIdx.x >> 6;
@@ -383,8 +383,8 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
   env_group<MODE, LPE>(cfg, env_offset, action, initial, st, ob, out, e, lane, s_oxa[wv] + grp * LPE,
-                       s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_ecura[wv] + grp * LPE,
-                       s_epreva[wv] + grp * LPE);
+                       s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_orra[wv] + grp * LPE,
+                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE);
 }
 
 // ============================================================================
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
                                                           ffmp_obs_t ob, ffmp_out_t out, int64_t sm_stride,
                                                           int64_t sm_frame, int32_t newest_only,
                                                           int32_t tile_log2r) {
-  __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST];
+  __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST], s_orr[FFMP_MAX_OBST];
   __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
   __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
@@ -873,7 +873,7 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   if (e >= n) return;
   if (threadIdx.x < 64)
     env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
-                                 s_ecur, s_eprev);
+                                 s_orr, s_ecur, s_eprev);
   // wave 0's record stores complete (write-through to the XCD's L2) before the barrier; the
   // waves below read them L1-bypassing (an agent-scope fence here would write back the L2)
   __threadfence_block();

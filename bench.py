@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--obs-format", default="f32", choices=["f32", "u8f16"],
                    help="f32: the reference consumer layout (state_m float32, the bench metric); u8f16: the "
                         "compact layout (uint8 frames, float16 potential) for consumers that convert on load")
+    p.add_argument("--compact-steps", type=int, default=100,
+                   help="N=1 f32 runs: also time this many steps of the same workload in the compact layout "
+                        "(obs_format=u8f16), reported as `compact_layout` beside the metric (0 = skip)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -152,6 +155,45 @@ def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool
         return float(d["raster_hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
         return None
+
+
+def time_compact(FFMPVec, name, cfg, n, dev, steps, warmup, seed):
+    """The same workload in the compact layout (uint8 frames, float16 potential; include/ffmp.h
+    FFMP_OBS_U8F16) on a fresh instance: whole-step rate and its raster's rate against HBM peak.
+    Not the metric (the reference consumer layout is float32), reported beside it."""
+    import torch
+    from flow_field_based_motion_planner_amd.config import bytes_per_env_step
+    env = FFMPVec(n, cfg, device=dev, obs_format="u8f16")
+    gen = torch.Generator(device=dev).manual_seed(2000 + seed)
+    actions = torch.randint(0, 28, (warmup + steps, n), device=dev, dtype=torch.int64, generator=gen)
+    env.reset()
+    for w in range(warmup):
+        env.step(actions[w])
+    torch.cuda.synchronize()
+    ep0 = int(env.episode.sum())
+    ev, t = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)), []
+    t0 = time.perf_counter()
+    ev[0].record()
+    for k in range(steps):
+        env.step(actions[warmup + k], timing=t)
+    ev[1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    resets = int(env.episode.sum()) - ep0
+    ms = [r[0].elapsed_time(r[1]) for r in t]
+    n_full = sum(1 for r in t if r[4])
+    byt = sum(r[3] for r in t) + resets * (len(t) - n_full) / len(t) * cfg.grid * cfg.grid
+    ach = byt / (sum(ms) * 1e-3) / 1e9
+    b = bytes_per_env_step(cfg, potential=True, window=env.frame_window, seamless=env.ring == "seamless",
+                           obs_format="u8f16")
+    out = {"obs_format": "u8f16", "value": n * steps / el, "unit": "env-steps/s", "steps": steps,
+           "ms_per_step": el * 1e3 / steps, "step_ms_events": ev[0].elapsed_time(ev[1]) / steps,
+           "kernel": "step_raster_kernel" if env.fused else "raster_kernel", "kernel_ms": sum(ms) / len(ms),
+           "achieved_gbs": ach, "frac": ach / PEAK_HBM_GBS, "bytes_per_env_step": b["total"],
+           "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
+           "shape": (env.placement or {}).get("shape_newest")}
+    env.close()
+    return out
 
 
 def main():
@@ -247,7 +289,18 @@ def main():
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
     per_launch_envs = raster_ev[0][2]
+    placement, env_fused, env_window, env_ring, env_slices = (env.placement, bool(env.fused), env.frame_window,
+                                                              env.ring, env.pipeline_slices)
     traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring, env.fused, args.obs_format)
+    compact = None
+    if world == 1 and args.obs_format == "f32" and args.compact_steps > 0 and not args.tuning \
+            and not args.no_potential and not args.flow:
+        env.close()
+        del env
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        compact = time_compact(FFMPVec, name, cfg, n, dev, args.compact_steps, 10, args.seed)
 
     if rank == 0:
         out = {
@@ -266,22 +319,24 @@ def main():
             "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
-                       "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
+                       "frame_window": env_window, "ring": env_ring, "fused": env_fused,
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
-                         "kernel": "step_raster_kernel" if env.fused else "raster_kernel", "kernel_ms": raster_ms,
+                         "kernel": "step_raster_kernel" if env_fused else "raster_kernel", "kernel_ms": raster_ms,
                          "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
                          "launches_per_step": len(r_ms) // K, "full_launches": n_full,
                          "timed_resets": resets},
             "raster_ms_per_step": sum(r_ms) / K,
             "step_ms_events": step_ms_ev,
-            "pipeline_slices": env.pipeline_slices,
-            "raster_autotune": env.placement,
+            "pipeline_slices": env_slices,
+            "raster_autotune": placement,
             "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
         }
+        if compact is not None:
+            out["compact_layout"] = compact
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             if args.cpu_procs > 0:

@@ -23,6 +23,7 @@ variants = {
     "footprint only": dict(collide_mode=1),
     "lidar only": dict(collide_mode=2),
     "G=64 (same K, L)": dict(grid=64),
+    "no resets": dict(collide_mode=0, max_steps=0, goal_thr=0.0),
 }
 only = sys.argv[1:]  # optional variant names to run
 for name, kw in variants.items():

@@ -22,9 +22,13 @@ constexpr double kTwoPi = 2.0 * 3.141592653589793;  // 2 * math.pi (train.py:169
 constexpr double kInv2p32 = 2.3283064365386962890625e-10;  // 2^-32
 
 // RobotAction.cmd (src/gym_ffmp/envs/robot/config.py:28-55): id = 7*vi + wi.
-// Stored as the literal lists, never computed (0.6 != 3*0.2 in binary).
-__constant__ double kCmdV[4] = {0.0, 0.2, 0.4, 0.6};
-__constant__ double kCmdW[7] = {-0.6, -0.4, -0.2, 0.0, 0.2, 0.4, 0.6};
+// The literal lists, never computed (0.6 != 3*0.2 in binary) — as selects over immediate
+// operands rather than a __constant__ table: a per-lane table index is a vector load, one more
+// dependent memory round trip at the head of the env step's latency chain.
+FFMP_DEV double cmd_v(int vi) { return vi == 0 ? 0.0 : vi == 1 ? 0.2 : vi == 2 ? 0.4 : 0.6; }
+FFMP_DEV double cmd_w(int wi) {
+  return wi == 0 ? -0.6 : wi == 1 ? -0.4 : wi == 2 ? -0.2 : wi == 3 ? 0.0 : wi == 4 ? 0.2 : wi == 5 ? 0.4 : 0.6;
+}
 
 // ROSNode.pi_to_pi (src/train.py:167-172): iterative wrap into (-pi, pi].
 // (+-inf would loop forever in the reference; returned unchanged here.)

@@ -65,6 +65,7 @@ int check_cfg(const ffmp_cfg_t* c) {
   if (c->n_foot < 0 || c->n_foot > FFMP_MAX_FOOT)
     return fail(FFMP_E_CFG, "n_foot out of range: %d", c->n_foot);
   if (c->n_beams > 0 && !c->beam_cs) return fail(FFMP_E_CFG, "beam_cs is NULL with n_beams > 0");
+  if (((uintptr_t)c->beam_cs & 15u) != 0) return fail(FFMP_E_CFG, "beam_cs must be 16-byte aligned");
   // the raster's sqrt_rn / rcp_rn are exact on this domain (ffmp_device.h)
   if (!(c->rho_min_f >= 0x1p-48f && c->rho_min_f <= 0x1p100f) || !(c->rho0_f <= 0x1p100f))
     return fail(FFMP_E_CFG, "rho_min must lie in [2^-48, 2^100] and rho0 <= 2^100");
@@ -136,6 +137,28 @@ FFMP_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Probe builds only (-DFFMP_TRACE, tools/gpu_trace.sh; never the shipped libffmp): wall-clock
+// stamps (100 MHz) at checkpoints of the env step (first 4096 envs, lane 0 of each env group)
+// and of the raster (first 65536 blocks, thread 0), read back by ffmp_trace_read.  Each stamp
+// first waits for the wave's outstanding memory operations, so the gaps are the chain's latency.
+#ifdef FFMP_TRACE
+__device__ uint64_t g_trace_env[4096 * 12];
+__device__ uint64_t g_trace_ras[65536 * 4];
+#define FFMP_ENV_STAMP(k)                                                   \
+  do {                                                                      \
+    __builtin_amdgcn_s_waitcnt(0);                                          \
+    if (lane == 0 && e < 4096) g_trace_env[e * 12 + (k)] = wall_clock64();   \
+  } while (0)
+#define FFMP_RAS_STAMP(k)                                                                     \
+  do {                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0);                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_trace_ras[blockIdx.x * 4 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define FFMP_ENV_STAMP(k) do {} while (0)
+#define FFMP_RAS_STAMP(k) do {} while (0)
+#endif
+
 // One env's raster record: header, goal, then K float4 of each of cur / prev / vel.
 // Lane k writes obstacle k; lanes 0..3 the header words.
 FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const FrameHdr& hc, const FrameHdr& hp,
@@ -159,6 +182,35 @@ FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const Fra
   }
 }
 
+// The lidar beam table {cos, sin} (cfg.beam_cs, (L, 2) float64) is read one beam ahead: lane
+// `lane` of a group serves beams lane, lane + LPE, ...; the load of the next beam is in flight
+// while the current one is traced, instead of a dependent round trip per beam.  first_beam is
+// issued at the top of the env step, so the first load overlaps the integrator.
+FFMP_DEV double2 first_beam(const ffmp_cfg_t& cfg, int lane) {
+  return lane < cfg.n_beams ? reinterpret_cast<const double2*>(cfg.beam_cs)[lane] : make_double2(0.0, 0.0);
+}
+
+template <class F>
+FFMP_DEV void for_beams(const ffmp_cfg_t& cfg, int lane, int lpe, double2 b, F&& f) {
+  const double2* bt = reinterpret_cast<const double2*>(cfg.beam_cs);
+  for (int l = lane; l < cfg.n_beams; l += lpe) {
+    const int ln = l + lpe;
+    const double2 nb = ln < cfg.n_beams ? bt[ln] : make_double2(0.0, 0.0);
+    f(l, b);
+    b = nb;
+  }
+}
+
+// The footprint offsets (cfg.foot_di / foot_dj) into the wave's LDS table, by every lane of the
+// wave before any lane leaves (call ahead of the kernel's early returns; env_group's wave_sync
+// orders it before the footprint test).  The kernel-argument segment is read uncached (~0.4 us a
+// load, measured): read in the footprint loop itself, one dependent round trip per offset made the
+// footprint 16 us of a C2 env step (profiles/r02_env_chain.txt); staged here, the loads of a wave
+// overlap each other and the state loads.
+FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, int2* s_foot) {
+  for (int f = (int)(threadIdx.x & 63); f < cfg.n_foot; f += 64) s_foot[f] = make_int2(cfg.foot_di[f], cfg.foot_dj[f]);
+}
+
 // LPE lanes per env (16, 32 or 64 >= K): a wave serves 64 / LPE envs, so the per-env scalar
 // float64 work (integrator, trig, goal, reward, record header) is issued once per 64/LPE envs
 // instead of once per env; lane k of an env's group holds its obstacle k, beams and footprint
@@ -171,13 +223,15 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
                                                        const ffmp_out_t& out, int64_t e, int lane, double* s_ox,
                                                        double* s_oy, double* s_or, double* s_orr, float4* s_ecur,
-                                                       float4* s_eprev) {
+                                                       float4* s_eprev, const int2* s_foot) {
   static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
   const int K = cfg.n_obst;
   const int L = cfg.n_beams;
   const int G = cfg.grid;
   const int ic = G / 2;
   const int64_t genv = env_offset + e;
+  FFMP_ENV_STAMP(0);
+  const double2 beam0 = first_beam(cfg, lane);  // in flight during the integrator's chain
 
   // ---- load (uniform scalars in every lane; obstacle k in lane k) ----
   double x0 = st.pose[e * 3 + 0], y0 = st.pose[e * 3 + 1], yaw0 = st.pose[e * 3 + 2];
@@ -208,7 +262,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       if (lane == 0) atomicOr(st.err, 1u);
       a = 3;  // (0.0, 0.0)
     }
-    const double v = kCmdV[a / 7], w = kCmdW[a % 7];
+    const double v = cmd_v((int)a / 7), w = cmd_w((int)a % 7);
     // ---- unicycle integrator (SPEC a15) ----
     c0 = cos(yaw0);
     s0 = sin(yaw0);
@@ -227,12 +281,15 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     vang = pi_to_pi(yaw1 - yaw0);
     t_obs = (float)cfg.dt;
   }
+  FFMP_ENV_STAMP(1);
 
   if (has_obst) lidar_disc(x1, y1, my.x, my.y, my.r, s_ox, s_oy, s_orr, s_or, lane);
   double c1 = cos(yaw1), s1 = sin(yaw1);
-  if (has_obst) s_ecur[lane] = ego_obst(my, x1, y1, c1, s1);
+  const float4 ecur1 = has_obst ? ego_obst(my, x1, y1, c1, s1) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (has_obst) s_ecur[lane] = ecur1;
   wave_sync();
 
+  FFMP_ENV_STAMP(2);
   FrameHdr hcur = make_hdr(x1, y1, c1, s1);
   FrameHdr hprev = (MODE == kEnvMode_Step) ? make_hdr(x0, y0, c0, s0) : hcur;
 
@@ -241,21 +298,27 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     const double dx = gx - x1, dy = gy - y1;
     const double dist = sqrt(dx * dx + dy * dy);
     // ---- collision: footprint on the current occupancy (ffmp.py:85-105) ----
+    // (cells in a wave-uniform loop over the offsets staged in LDS by stage_footprint, discs
+    // lane-parallel: lane k tests its disc k, lane 0 the walls; the ballot below ORs them:
+    // occupied_cell's value for every cell)
     bool c_foot = false;
     if (cfg.collide_mode & FFMP_COLLIDE_FOOTPRINT) {
-      for (int f = lane; f < cfg.n_foot; f += LPE)
-        c_foot |= occupied_cell(cfg, hcur, s_ecur, K, ic + cfg.foot_di[f], ic + cfg.foot_dj[f]);
+      for (int f = 0; f < cfg.n_foot; ++f) {
+        const int2 fo = s_foot[f];
+        const float ex = cell_coord(cfg, ic + fo.x), ey = cell_coord(cfg, ic + fo.y);
+        c_foot |= (has_obst && in_disc(ex, ey, ecur1)) || (lane == 0 && outside_world(cfg, hcur, ex, ey));
+      }
     }
+    FFMP_ENV_STAMP(7);
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    for (int l = lane; l < L; l += LPE) {
-      const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_orr, s_or);
-      const float rf = (float)r;
+    for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
+      const float rf = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
       ob.lidar[e * L + l] = rf;
       c_lidar |= beam_collides(rf, cfg.robot_r);
-    }
+    });
+    FFMP_ENV_STAMP(8);
     c_foot = group_ballot(c_foot, LPE) != 0;
     c_lidar = (group_ballot(c_lidar, LPE) != 0) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
     col = c_foot || c_lidar;
@@ -277,11 +340,13 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
         to[0] = g0; to[1] = g1; to[2] = (float)vlin; to[3] = (float)vang; to[4] = t_obs;
       }
     }
+    FFMP_ENV_STAMP(9);
     if (reset_now && st.term_record)  // the terminal state, before the reset below overwrites it
       write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev,
                    to_ego(gx, gy, x1, y1, c1, s1), s_ecur[lane], s_eprev[lane], ego_vel(my, c1, s1), 0.0f);
   }
 
+  FFMP_ENV_STAMP(3);
   if (reset_now) {
     // ---- episode reset (the external /episode_manager; train.py:559-566) ----
     episode = (MODE == kEnvMode_Reset && initial) ? 0 : episode + 1;
@@ -310,13 +375,12 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    for (int l = lane; l < L; l += LPE) {
-      const double r = lidar_beam(cfg, sc, x1, y1, c1, s1, cfg.beam_cs[2 * l], cfg.beam_cs[2 * l + 1],
-                                  s_ox, s_oy, s_orr, s_or);
-      ob.lidar[e * L + l] = (float)r;
-    }
+    for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
+      ob.lidar[e * L + l] = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
+    });
   }
 
+  FFMP_ENV_STAMP(4);
   // ---- field-gradient lookup at the robot cell (central differences) ----
   {
     const float2 ge = to_ego(gx, gy, x1, y1, c1, s1);
@@ -341,6 +405,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
   }
 
+  FFMP_ENV_STAMP(5);
   // ---- write back state / obs / outputs ----
   if (has_obst) {
     double* p = st.obst + (e * K + lane) * 4;
@@ -364,6 +429,7 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       out.truncated[e] = trunc;
     }
   }
+  FFMP_ENV_STAMP(6);
 }
 
 template <int MODE, int kEnvWaves, int LPE>
@@ -375,16 +441,18 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
   __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
       s_ora[kEnvWaves][FFMP_MAX_OBST], s_orra[kEnvWaves][FFMP_MAX_OBST];
   __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
+  __shared__ int2 s_foota[kEnvWaves][FFMP_MAX_FOOT];
 
   const int wv = threadIdx.x >> 6;
   const int grp = (threadIdx.x & 63) / LPE;
   const int64_t e = ((int64_t)blockIdx.x * kEnvWaves + wv) * EPW + grp;
   const int lane = threadIdx.x & (LPE - 1);  // lane within the env's group
+  if (MODE == kEnvMode_Step) stage_footprint(cfg, s_foota[wv]);
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
   env_group<MODE, LPE>(cfg, env_offset, action, initial, st, ob, out, e, lane, s_oxa[wv] + grp * LPE,
                        s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_orra[wv] + grp * LPE,
-                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE);
+                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE, s_foota[wv]);
 }
 
 // ============================================================================
@@ -531,6 +599,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   const int G = cfg.grid;
   const int G2 = G * G;
   const int tid = threadIdx.x;
+  FFMP_RAS_STAMP(0);
   const float* rec = record + e * rec_stride(K);
   if (tid < FFMP_REC_HDR) s_hdr[tid] = rec_word<FRESH>(rec + tid);
   if (tid < K) {
@@ -543,6 +612,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
     }
   }
   __syncthreads();
+  FFMP_RAS_STAMP(1);
 
   const FrameHdr hc{s_hdr[0], s_hdr[1], s_hdr[2], s_hdr[3]};
   const FrameHdr hp{s_hdr[4], s_hdr[5], s_hdr[6], s_hdr[7]};
@@ -851,6 +921,10 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
   if (mask && !mask[e]) return;
   raster_env<NT, FLOW, FMT>(cfg, e, tile, cells_per_block, record, state_m, sm_stride, sm_frame, newest_only, pot, flow,
                        tile_log2r, s_cur, s_prev, s_vel, s_hdr);
+#ifdef FFMP_TRACE
+  __syncthreads();
+  FFMP_RAS_STAMP(2);
+#endif
 }
 
 // The fused step: one block per env.  Wave 0 steps the env (env_group, 64 lanes: integrator,
@@ -866,14 +940,17 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
                                                           int32_t tile_log2r) {
   __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST], s_orr[FFMP_MAX_OBST];
   __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
+  __shared__ int2 s_foot[FFMP_MAX_FOOT];
   __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
   __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
   __shared__ float s_hdr[FFMP_REC_HDR];
   const int64_t e = logical_block<XCD>();
   if (e >= n) return;
-  if (threadIdx.x < 64)
+  if (threadIdx.x < 64) {
+    stage_footprint(cfg, s_foot);
     env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
-                                 s_orr, s_ecur, s_eprev);
+                                 s_orr, s_ecur, s_eprev, s_foot);
+  }
   // wave 0's record stores complete (write-through to the XCD's L2) before the barrier; the
   // waves below read them L1-bypassing (an agent-scope fence here would write back the L2)
   __threadfence_block();
@@ -1464,4 +1541,19 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
   return check_launch("ffmp_episode_update");
 }
 
+#ifdef FFMP_TRACE
+// Probe builds only: copy the stamps (env: 4096 x 12, raster: 65536 x 4 uint64) to host memory.
+int ffmp_trace_read(uint64_t* env_host, uint64_t* ras_host, int clear) {
+  if (hipMemcpyFromSymbol(env_host, HIP_SYMBOL(g_trace_env), sizeof(uint64_t) * 4096 * 12) != hipSuccess ||
+      hipMemcpyFromSymbol(ras_host, HIP_SYMBOL(g_trace_ras), sizeof(uint64_t) * 65536 * 4) != hipSuccess)
+    return fail(FFMP_E_HIP, "ffmp_trace_read: copy failed");
+  if (clear) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace_env)) != hipSuccess || hipMemset(p, 0, sizeof(uint64_t) * 4096 * 12) != hipSuccess ||
+        hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace_ras)) != hipSuccess || hipMemset(p, 0, sizeof(uint64_t) * 65536 * 4) != hipSuccess)
+      return fail(FFMP_E_HIP, "ffmp_trace_read: clear failed");
+  }
+  return hipDeviceSynchronize() == hipSuccess ? FFMP_OK : fail(FFMP_E_HIP, "ffmp_trace_read: sync failed");
+}
+#endif
 }  // extern "C"

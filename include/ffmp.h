@@ -100,7 +100,7 @@ typedef struct ffmp_cfg {
   float inv_2res_f;      /* (float)(1.0 / (2.0 * res)) : central-difference scale */
   float cull_margin_f;   /* extra culling margin (m), conservative */
   uint64_t seed;         /* Philox4x32-10 key */
-  const double* beam_cs; /* DEVICE (L,2) float64 {cos, sin} of beam angle -pi + l*2pi/L */
+  const double* beam_cs; /* DEVICE (L,2) float64 {cos, sin} of beam angle -pi + l*2pi/L, 16-B aligned */
 } ffmp_cfg_t;
 
 /* Per-env simulator state (device pointers, N envs). */

@@ -1,5 +1,6 @@
-"""Where the env kernel's time goes at C3 size: time ffmp_step_state alone for variants of the
-C3 config (no lidar, no obstacles, static obstacles, footprint-only collisions, fewer beams)."""
+"""Where the env kernel's time goes: time ffmp_step_state alone for variants of a preset (no lidar,
+no obstacles, static obstacles, footprint-only collisions, fewer beams, no resets).
+usage: python tools/env_kernel_breakdown.py [--preset C3] [--envs 32768] [variant ...]"""
 import gc
 import os
 import sys
@@ -10,9 +11,16 @@ import torch  # noqa: E402
 from flow_field_based_motion_planner_amd.config import preset  # noqa: E402
 from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 
-n = 32768
+args = sys.argv[1:]
+base, n = "C3", 32768
+while args and args[0].startswith("--"):
+    if args[0] == "--preset":
+        base = args[1]
+    elif args[0] == "--envs":
+        n = int(args[1])
+    args = args[2:]
 variants = {
-    "C3": {},
+    "base": {},
     "L=0 (no lidar)": dict(n_beams=0),
     "L=64": dict(n_beams=64),
     "K=0": dict(n_obst=0),
@@ -25,11 +33,11 @@ variants = {
     "G=64 (same K, L)": dict(grid=64),
     "no resets": dict(collide_mode=0, max_steps=0, goal_thr=0.0),
 }
-only = sys.argv[1:]  # optional variant names to run
+only = args  # optional variant names to run
 for name, kw in variants.items():
     if only and name not in only:
         continue
-    env = FFMPVec(n, preset("C3", **kw), device="cuda:0", autotune=False, frame_window=2, potential=False)
+    env = FFMPVec(n, preset(base, **kw), device="cuda:0", autotune=False, frame_window=2, potential=False)
     env.reset()
     acts = torch.randint(0, 28, (60, n), device="cuda:0")
     for k in range(10):
@@ -41,7 +49,7 @@ for name, kw in variants.items():
         env.step_state(acts[k])
     ev[1].record()
     torch.cuda.synchronize()
-    print(f"{name:20s}: env kernel {ev[0].elapsed_time(ev[1]) / 50 * 1000:7.1f} us", flush=True)
+    print(f"{base} n={n} {name:20s}: env kernel {ev[0].elapsed_time(ev[1]) / 50 * 1000:7.1f} us", flush=True)
     del env
     gc.collect()
     torch.cuda.empty_cache()

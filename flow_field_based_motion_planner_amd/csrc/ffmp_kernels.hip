@@ -529,6 +529,9 @@ FFMP_DEV void store4_h(_Float16* p, float a, float b, float c, float d) {
   else *reinterpret_cast<f16x4*>(p) = v;
 }
 
+// A wave-uniform float moved to a scalar register.
+FFMP_DEV float uni(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
 FFMP_DEV float box_dist2(float px, float py, float x0, float x1, float y0, float y1) {
   const float dx = fmaxf(fmaxf(x0 - px, px - x1), 0.0f);
   const float dy = fmaxf(fmaxf(y0 - py, py - y1), 0.0f);
@@ -614,12 +617,17 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   __syncthreads();
   FFMP_RAS_STAMP(1);
 
-  const FrameHdr hc{s_hdr[0], s_hdr[1], s_hdr[2], s_hdr[3]};
-  const FrameHdr hp{s_hdr[4], s_hdr[5], s_hdr[6], s_hdr[7]};
-  const float gx = s_hdr[8], gy = s_hdr[9];
+  // The header is block-uniform.  FMT_CT4: keep it in scalar registers (readfirstlane) instead of
+  // 11 VGPRs — 108 -> 72 VGPRs, 4 -> 7 waves per SIMD, compact C3 raster 1.15-1.29 -> 1.00-1.13 ms
+  // (profiles/r02_occupancy.txt).  Not for the float32 layout (store-bound: 7 waves per SIMD ran
+  // its steps ~2 % slower than 4) nor for FMT_CT16 (the scheduler then took 188 VGPRs, not 167).
+  auto hv = [&](int i) { return FMT == FMT_CT4 ? uni(s_hdr[i]) : s_hdr[i]; };
+  const FrameHdr hc{hv(0), hv(1), hv(2), hv(3)};
+  const FrameHdr hp{hv(4), hv(5), hv(6), hv(7)};
+  const float gx = hv(8), gy = hv(9);
   // temporal stack in place: the older frame already holds the previous newest one unless this
   // env was reset (block-uniform)
-  const bool write_old = !newest_only || s_hdr[10] != 0.0f;
+  const bool write_old = !newest_only || hv(10) != 0.0f;
   const float res = cfg.res_f, half = cfg.half_f;
   const float invG = 1.0f / (float)G;
 

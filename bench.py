@@ -191,7 +191,9 @@ def time_compact(FFMPVec, name, cfg, n, dev, steps, warmup, seed):
            "kernel": "step_raster_kernel" if env.fused else "raster_kernel", "kernel_ms": sum(ms) / len(ms),
            "achieved_gbs": ach, "frac": ach / PEAK_HBM_GBS, "bytes_per_env_step": b["total"],
            "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
-           "shape": (env.placement or {}).get("shape_newest")}
+           "shape": (env.placement or {}).get("shape_newest"),
+           "ring_pairing": {k: (env.ring_meta or {}).get(k) for k in ("pieces", "pair_probes", "pair_gbs_min",
+                                                                        "pair_gbs_max", "rebuilds", "reverts")}}
     env.close()
     return out
 

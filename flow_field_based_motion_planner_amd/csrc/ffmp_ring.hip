@@ -31,7 +31,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //   same pages pair identically; tools/region_probe.hip), so one slot that pairs badly with
 //   the potential plane makes one step in W ~25 % slower.  With a `partner` (the potential
 //   plane), every piece position (slot i, piece j) gets a piece measured to pair well with the
-//   partner's bytes [j*P, (j+1)*P): a two-stream store probe, candidates from the free-piece
+//   partner's bytes the raster writes beside it — [j*P, (j+1)*P) in the float32 layout,
+//   [2j*P, 2(j+1)*P) for compact uint8 frames beside a binary16 plane (the ratio of partner
+//   bytes to slot bytes, RingGeom::scale) — by a two-stream store probe of the same byte ratio,
+//   candidates from the free-piece
 //   pool first, then fresh pieces; pieces that pair badly here stay pooled for other positions
 //   or later rings.
 // * Never unmap.  Once a VMM range is unmapped and its address reused by a new mapping, the
@@ -91,12 +94,21 @@ struct DLHolder_ {  // one allocation: the managed tensor, its shape/strides, it
   ffmp_ring* owner;
 };
 
-// two lockstep 16-B nontemporal store streams over n16 float4s: the raster's write pattern
+// two lockstep 16-B nontemporal store streams, n16 float4s to `a` and SCALE x n16 to `b`: the
+// raster's write pattern (float32 layout: frame and potential plane at the same rate, SCALE 1;
+// compact layout: 1-byte frame cells beside 2-byte potential cells, SCALE 2)
+// (every store instruction of a wave covers 1 KiB of contiguous bytes of its stream; n16 is a
+// multiple of 4096: pieces are >= 256 MiB)
+template <int SCALE>
 __global__ __launch_bounds__(256) void pair_probe_kernel(f32x4* __restrict__ a, f32x4* __restrict__ b, int64_t n16) {
-  for (int64_t i = (int64_t)blockIdx.x * 4096 + threadIdx.x; i < n16 && i < ((int64_t)blockIdx.x + 1) * 4096; i += 256) {
-    const f32x4 x = {0.f, 1.f, 2.f, 3.f};
+  const int64_t blk0 = (int64_t)blockIdx.x * 4096;
+  const f32x4 x = {0.f, 1.f, 2.f, 3.f};
+  for (int k = 0; k < 16; ++k) {
+    const int64_t i = blk0 + threadIdx.x + 256 * k;
+    if (i >= n16) break;
     __builtin_nontemporal_store(x, a + i);
-    __builtin_nontemporal_store(x, b + i);
+#pragma unroll
+    for (int s = 0; s < SCALE; ++s) __builtin_nontemporal_store(x, b + SCALE * blk0 + threadIdx.x + 256 * (SCALE * k + s));
   }
 }
 
@@ -105,7 +117,7 @@ namespace {
 std::mutex g_pool_mu;
 std::vector<ffmp_piece> g_pieces;   // free pieces (mapped at home), reusable
 std::vector<ffmp_piece> g_retired;  // free, but GPU work issued before their ring died may still write them
-std::atomic<double> g_ref_gbs[64];  // best pairing probe seen per device (choose_pieces)
+std::atomic<double> g_ref_gbs[64][2];  // best pairing probe seen per device and partner scale 1 / 2 (choose_pieces)
 
 hipMemAllocationProp dev_prop(int32_t device) {
   hipMemAllocationProp prop = {};
@@ -155,21 +167,24 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
   return hipSuccess;
 }
 
-// GB/s of the two-stream store probe over `bytes` of piece home + partner range
-double pair_gbs(char* a, char* b, size_t bytes, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+// GB/s of the two-stream store probe over `bytes` of piece home + scale x `bytes` of partner
+double pair_gbs(char* a, char* b, size_t bytes, int scale, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int64_t n16 = (int64_t)(bytes / 16);
   const unsigned blocks = (unsigned)((n16 + 4095) / 4096);
   float best = 1e30f;
   for (int r = 0; r < 4; ++r) {
     (void)hipEventRecord(e0, s);
-    hipLaunchKernelGGL(pair_probe_kernel, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
+    if (scale == 2)
+      hipLaunchKernelGGL(pair_probe_kernel<2>, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
+    else
+      hipLaunchKernelGGL(pair_probe_kernel<1>, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
     (void)hipEventRecord(e1, s);
     if (hipEventSynchronize(e1) != hipSuccess) return 0.0;
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
     if (r > 0 && ms < best) best = ms;  // first launch warms up
   }
-  return 2.0 * (double)(n16 * 16) / (best * 1e-3) / 1e9;
+  return (1.0 + scale) * (double)(n16 * 16) / (best * 1e-3) / 1e9;
 }
 
 void ring_unref(ffmp_ring* r) {
@@ -202,9 +217,10 @@ struct RingGeom {
   size_t gran, piece, stride;
   int per_slot;
   bool pairing;
+  int scale;  // partner bytes per slot byte the raster writes in lockstep: 1 (float32 layout) or 2 (compact)
 };
 
-int ring_geom(int32_t device, int64_t slot_bytes, const void* partner, RingGeom* g) {
+int ring_geom(int32_t device, int64_t slot_bytes, const void* partner, int64_t partner_bytes, RingGeom* g) {
   int vmm = 0;
   if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
     return fail(FFMP_E_HIP, "ffmp_ring: device %d has no virtual memory management", device);
@@ -217,6 +233,10 @@ int ring_geom(int32_t device, int64_t slot_bytes, const void* partner, RingGeom*
   g->per_slot = (int)((slot_g + g->piece - 1) / g->piece);
   g->stride = g->piece * (size_t)g->per_slot;
   g->pairing = partner != nullptr && g->piece >= (256ull << 20);
+  // The raster writes cell q of a slot and of the partner (the potential plane) in lockstep: the
+  // same byte offset in the float32 layout, twice the offset for compact uint8 frames beside a
+  // binary16 plane — the ratio of the plane to one slot (rounded: a rebuild passes the stride).
+  g->scale = partner && partner_bytes >= (int64_t)(1.5 * (double)slot_bytes) ? 2 : 1;
   return FFMP_OK;
 }
 
@@ -240,7 +260,7 @@ bool room_for(size_t bytes) {
 
 // Fill r->pieces[pos] for every pos with need[pos] set: candidates from the pool first (at most
 // 6 per position), then fresh pieces; with a partner, the first piece whose two-stream store
-// probe against the partner bytes at the same offset is within 7 % of the best probe seen
+// probe against the partner bytes written beside it is within 7 % of the best probe seen
 // (after >= 3 probes), else the best of 12.  Pieces held by a ring are never candidates.
 int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
                   int64_t partner_bytes) {
@@ -282,16 +302,19 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
   int todo = 0;
   for (char n : need) todo += n != 0;
   const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
-  double ref = g_ref_gbs[device & 63].load(std::memory_order_relaxed);      // best probe seen on the device: the scale "fast" is judged against
+  std::atomic<double>& ref_slot = g_ref_gbs[device & 63][g.scale == 2 ? 1 : 0];
+  double ref = ref_slot.load(std::memory_order_relaxed);      // best probe seen on the device: the scale "fast" is judged against
   bool found_fast = false;
   int fresh = 0;
   hipError_t e = hipSuccess;
   for (size_t pos = 0; pos < need.size(); ++pos) {
     if (!need[pos]) continue;
     const int j = (int)(pos % (size_t)g.per_slot);
-    const size_t off = (size_t)j * g.piece;
+    const size_t off = (size_t)j * g.piece * (size_t)g.scale;  // the partner bytes written beside piece j
     char* pb = g.pairing ? (char*)partner + off : nullptr;
-    const size_t pbytes = g.pairing && (int64_t)off < partner_bytes ? std::min(g.piece, (size_t)(partner_bytes - (int64_t)off)) : 0;
+    // slot bytes of piece j that have partner bytes beside them (the probe writes scale x these)
+    const size_t pbytes = g.pairing && (int64_t)off < partner_bytes
+                              ? std::min(g.piece, (size_t)(partner_bytes - (int64_t)off) / (size_t)g.scale) : 0;
     // no probe has found a fast pair in the first 12: the partner sits where nothing pairs
     // well (seen at C5), so stop paying for probes and extra pieces
     const bool test = g.pairing && pbytes >= (64u << 20) && (found_fast || r->pieces_tested < 12);
@@ -321,13 +344,13 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
         pick = c;
         break;
       }
-      const double gbs = pair_gbs(cand[c].home, pb, pbytes, s, e0, e1);
+      const double gbs = pair_gbs(cand[c].home, pb, pbytes, g.scale, s, e0, e1);
       ++r->pieces_tested;
       ++here;
       if (gbs >= kPairFastGBs) found_fast = true;
       if (gbs > ref) {
         ref = gbs;
-        g_ref_gbs[device & 63].store(gbs, std::memory_order_relaxed);
+        ref_slot.store(gbs, std::memory_order_relaxed);
       }
       if (gbs > pick_gbs) {
         pick = c;
@@ -385,7 +408,7 @@ int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const vo
   if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_create: partner_bytes must be > 0");
   DeviceScope scope(device);
   RingGeom g;
-  if (const int rc = ring_geom(device, slot_bytes, partner, &g)) return rc;
+  if (const int rc = ring_geom(device, slot_bytes, partner, partner_bytes, &g)) return rc;
   std::unique_ptr<ffmp_ring> r(new ffmp_ring());
   r->device = device;
   r->slots = slots;
@@ -415,7 +438,7 @@ int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partn
   if (partner && partner_bytes <= 0) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: partner_bytes must be > 0");
   DeviceScope scope(old->device);
   RingGeom g;
-  if (const int rc = ring_geom(old->device, (int64_t)old->stride, partner, &g)) return rc;
+  if (const int rc = ring_geom(old->device, (int64_t)old->stride, partner, partner_bytes, &g)) return rc;
   if (g.stride != old->stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: geometry changed");
   std::unique_ptr<ffmp_ring> r(new ffmp_ring());
   r->device = old->device;

@@ -333,8 +333,10 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
  *   partner (optional, device pointer, partner_bytes): the plane the raster writes in lockstep
  *   with every slot (the potential plane).  Two lockstep store streams run ~25 % slower when
  *   their physical pages pair badly, so each piece position gets a piece measured (two-stream
- *   store probe, which overwrites the partner's bytes) to pair well with the partner bytes at
- *   the same offset.  NULL: no pairing.
+ *   store probe, which overwrites the partner's bytes) to pair well with the partner bytes the
+ *   raster writes beside it: the same offset when partner_bytes < 1.5 x slot_bytes (float32
+ *   frames beside a float32 plane), twice the offset otherwise (uint8 frames beside a binary16
+ *   plane, FFMP_OBS_U8F16).  NULL: no pairing.
  *   *base = the first virtual slot (device pointer); contents undefined.
  * Returns 0, FFMP_E_ARG, or FFMP_E_HIP (no VMM support, out of memory, ...; then use a plain
  * ring — ffmp_last_error() says which call failed).

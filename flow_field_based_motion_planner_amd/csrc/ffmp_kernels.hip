@@ -14,6 +14,7 @@
 //   reward_done_kernel / footprint_kernel / scan_kernel — legacy FFMP methods.
 // The seamless frame ring (HIP virtual memory) and the DLPack hand-off: ffmp_ring.hip.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <type_traits>
 #include <math.h>
 #include <stdio.h>
@@ -95,6 +96,7 @@ struct Tuning {
   int xcd_remap = 0;           // 1: each XCD walks its own contiguous range of (env, tile) blocks
   int env_waves = 1;           // waves per env_kernel block: 1 or 4
   int env_lanes = 0;           // lanes per env: 0 = auto (>= K, more for many lidar beams)
+  int lds_pad = 0;             // probe only (FFMP_RASTER_LDS_PAD): dynamic LDS bytes per raster block, to cap its occupancy
 };
 
 Tuning& tuning() {
@@ -107,6 +109,7 @@ Tuning& tuning() {
     if (const char* v = getenv("FFMP_RASTER_NT")) r.nontemporal = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("FFMP_RASTER_XCD")) r.xcd_remap = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("FFMP_ENV_WAVES")) r.env_waves = atoi(v) == 4 ? 4 : 1;
+    if (const char* v = getenv("FFMP_RASTER_LDS_PAD")) r.lds_pad = std::max(0, std::min(atoi(v), 65536));
     if (const char* v = getenv("FFMP_ENV_LANES")) {
       const int l = atoi(v);
       r.env_lanes = (l == 16 || l == 32 || l == 64) ? l : 0;
@@ -1402,7 +1405,7 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
     float* pot = obs->potential ? (float*)((char*)obs->potential + e0 * (int64_t)G2 * (ct ? 2 : 4)) : nullptr;
     float* flw = obs->flow ? obs->flow + e0 * 2 * (int64_t)G2 : nullptr;
     dispatch_variant(fmt, nt, xcd, fl, [&](auto NT_, auto XCD_, auto FL_, auto FMT_) {
-      hipLaunchKernelGGL((raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, 0, s, *cfg, m,
+      hipLaunchKernelGGL((raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, tuning().lds_pad, s, *cfg, m,
                          bpe, cpb, rec, msk, sm, sm_stride, sm_frame, newest, pot, flw, tile_log2r);
     });
     if (int rc2 = check_launch("ffmp_raster")) return rc2;
@@ -1465,7 +1468,7 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
   hipStream_t s = (hipStream_t)stream;
   ffmp_out_t o = *out;
   dispatch_variant(fmt, nt, xcd, fl, [&](auto NT_, auto XCD_, auto FL_, auto FMT_) {
-    hipLaunchKernelGGL((step_raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, 0, s, *cfg, n,
+    hipLaunchKernelGGL((step_raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, tuning().lds_pad, s, *cfg, n,
                        env_offset, action, *state, *obs, o, sm_stride, sm_frame, newest, tile_log2r);
   });
   return check_launch("ffmp_step_fused");

@@ -64,6 +64,11 @@ def test_argument_validation_no_gpu(lib):
     assert lib.ffmp_raster(C.byref(bad), 1, None, None, C.byref(ob), None) == -3
     lidar_cfg = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=8))  # beam_cs NULL
     assert lib.ffmp_reset(C.byref(lidar_cfg), 1, 0, None, 1, C.byref(st), C.byref(ob), None) == -3
+    table = (C.c_double * 40)()  # the beam table is read as 16-B {cos, sin} pairs: 8-B aligned is refused
+    base = C.cast(table, C.c_void_p).value
+    lidar_cfg.beam_cs = base + (8 if base % 16 == 0 else 0)
+    assert lib.ffmp_reset(C.byref(lidar_cfg), 1, 0, None, 1, C.byref(st), C.byref(ob), None) == -3
+    assert b"16-byte aligned" in lib.ffmp_last_error()
     assert lib.ffmp_scan_collision(-1, 4, None, 0.13, None, None, None) == -1
     # n == 0 with valid pointers is a no-op success (no launch)
     dummy = (C.c_double * 8)()

@@ -226,7 +226,8 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
                                                        const ffmp_out_t& out, int64_t e, int lane, double* s_ox,
                                                        double* s_oy, double* s_or, double* s_orr, float4* s_ecur,
-                                                       float4* s_eprev, const int2* s_foot) {
+                                                       float4* s_eprev, const int2* s_foot, float* s_rhdr = nullptr,
+                                                       float2* s_rvel = nullptr) {
   static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
   const int K = cfg.n_obst;
   const int L = cfg.n_beams;
@@ -404,6 +405,14 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     const float4 vel = ego_vel(my, c1, s1);
     write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel,
                  reset_now ? 1.0f : 0.0f);
+    if (s_rhdr) {  // the one-launch step: the record's header (and velocities) for the block's raster, in LDS
+      if (lane < FFMP_REC_HDR) {
+        const float hv[FFMP_REC_HDR] = {hcur.px, hcur.py, hcur.c, hcur.s, hprev.px, hprev.py, hprev.c, hprev.s,
+                                        ge.x,    ge.y,    reset_now ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        s_rhdr[lane] = hv[lane];
+      }
+      if (s_rvel && has_obst) s_rvel[lane] = make_float2(vel.x, vel.y);
+    }
     if (MODE == kEnvMode_Step && !reset_now && st.term_record)
       write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
   }
@@ -567,19 +576,6 @@ FFMP_DEV int64_t logical_block() {
   return lb;
 }
 
-// A record word.  FRESH: the record was written earlier in this launch (by wave 0 of the block,
-// step_raster_kernel): load it device-coherently (bypassing the CU's vector L1, which may hold
-// a line shared with a neighbouring env's record read by another block on the CU).
-template <bool FRESH>
-FFMP_DEV float rec_word(const float* p) {
-  if (FRESH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return *p;
-}
-
-template <bool FRESH>
-FFMP_DEV float4 rec_word4(const float* p) {
-  return make_float4(rec_word<FRESH>(p), rec_word<FRESH>(p + 1), rec_word<FRESH>(p + 2), rec_word<FRESH>(p + 3));
-}
 
 // Observation format of a raster instantiation: FMT_F32 (reference layout), FMT_CT4 (compact
 // FFMP_OBS_U8F16, 4 cells per lane) or FMT_CT16 (compact, 16 cells per lane: a wave task is
@@ -590,7 +586,9 @@ constexpr int FMT_F32 = 0, FMT_CT4 = 1, FMT_CT16 = 2;
 // The raster of cells [tile * cells_per_block, ...) of env e by the whole 256-thread block
 // (block-uniform arguments; contains a block barrier).  Compact formats: state_m holds uint8
 // frames and pot binary16 planes (the pointers are reinterpreted; strides in elements).
-template <bool NT, bool FLOW, int FMT, bool FRESH = false>
+// PRELOADED: the record is already in the block's LDS (s_hdr, s_cur, s_prev, s_vel; written by the
+// one-launch step's env_group before a block barrier), so the raster does not read it back from HBM.
+template <bool NT, bool FLOW, int FMT, bool PRELOADED = false>
 FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, int64_t e, int tile, int32_t cells_per_block,
                                                         const float* __restrict__ record,
                                                         float* __restrict__ state_m, int64_t sm_stride,
@@ -607,17 +605,18 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   const int tid = threadIdx.x;
   FFMP_RAS_STAMP(0);
   const float* rec = record + e * rec_stride(K);
-  if (tid < FFMP_REC_HDR) s_hdr[tid] = rec_word<FRESH>(rec + tid);
-  if (tid < K) {
-    const float* ro = rec + FFMP_REC_HDR;
-    s_cur[tid] = rec_word4<FRESH>(ro + 4 * tid);
-    s_prev[tid] = rec_word4<FRESH>(ro + 4 * (K + tid));
-    if (FLOW) {
-      const float4 v = rec_word4<FRESH>(ro + 4 * (2 * K + tid));
-      s_vel[tid] = make_float2(v.x, v.y);
+  if (!PRELOADED) {
+    if (tid < FFMP_REC_HDR) s_hdr[tid] = rec[tid];
+    if (tid < K) {
+      const float* ro = rec + FFMP_REC_HDR;  // 4-B words: the ABI asks no more alignment of the record
+      const float* c = ro + 4 * tid;
+      const float* q = ro + 4 * (K + tid);
+      s_cur[tid] = make_float4(c[0], c[1], c[2], c[3]);
+      s_prev[tid] = make_float4(q[0], q[1], q[2], q[3]);
+      if (FLOW) s_vel[tid] = make_float2(ro[4 * (2 * K + tid)], ro[4 * (2 * K + tid) + 1]);
     }
+    __syncthreads();
   }
-  __syncthreads();
   FFMP_RAS_STAMP(1);
 
   // The header is block-uniform.  FMT_CT4: keep it in scalar registers (readfirstlane) instead of
@@ -952,7 +951,6 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST], s_orr[FFMP_MAX_OBST];
   __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
   __shared__ int2 s_foot[FFMP_MAX_FOOT];
-  __shared__ float4 s_cur[FFMP_MAX_OBST], s_prev[FFMP_MAX_OBST];
   __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
   __shared__ float s_hdr[FFMP_REC_HDR];
   const int64_t e = logical_block<XCD>();
@@ -960,14 +958,14 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   if (threadIdx.x < 64) {
     stage_footprint(cfg, s_foot);
     env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
-                                 s_orr, s_ecur, s_eprev, s_foot);
+                                 s_orr, s_ecur, s_eprev, s_foot, s_hdr, FLOW ? s_vel : nullptr);
   }
-  // wave 0's record stores complete (write-through to the XCD's L2) before the barrier; the
-  // waves below read them L1-bypassing (an agent-scope fence here would write back the L2)
-  __threadfence_block();
+  // The record reaches the raster through LDS: env_group left its ego discs of both frames in
+  // s_ecur / s_eprev and wrote the header (and velocities) to s_hdr / s_vel — the same words it
+  // stored to st.record — so the raster starts without a round trip to HBM for them.
   __syncthreads();
   raster_env<NT, FLOW, FMT, true>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
-                       ob.potential, ob.flow, tile_log2r, s_cur, s_prev, s_vel, s_hdr);
+                       ob.potential, ob.flow, tile_log2r, s_ecur, s_eprev, s_vel, s_hdr);
 }
 
 // ============================================================================

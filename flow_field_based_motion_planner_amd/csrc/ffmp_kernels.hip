@@ -603,7 +603,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   const int G = cfg.grid;
   const int G2 = G * G;
   const int tid = threadIdx.x;
-  FFMP_RAS_STAMP(0);
+  if (!PRELOADED) FFMP_RAS_STAMP(0);
   const float* rec = record + e * rec_stride(K);
   if (!PRELOADED) {
     if (tid < FFMP_REC_HDR) s_hdr[tid] = rec[tid];
@@ -617,7 +617,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
     }
     __syncthreads();
   }
-  FFMP_RAS_STAMP(1);
+  if (!PRELOADED) FFMP_RAS_STAMP(1);
 
   // The header is block-uniform.  FMT_CT4: keep it in scalar registers (readfirstlane) instead of
   // 11 VGPRs — 108 -> 72 VGPRs, 4 -> 7 waves per SIMD, compact C3 raster 1.15-1.29 -> 1.00-1.13 ms
@@ -955,6 +955,7 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   __shared__ float s_hdr[FFMP_REC_HDR];
   const int64_t e = logical_block<XCD>();
   if (e >= n) return;
+  FFMP_RAS_STAMP(0);
   if (threadIdx.x < 64) {
     stage_footprint(cfg, s_foot);
     env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
@@ -964,8 +965,13 @@ __global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_
   // s_ecur / s_eprev and wrote the header (and velocities) to s_hdr / s_vel — the same words it
   // stored to st.record — so the raster starts without a round trip to HBM for them.
   __syncthreads();
+  FFMP_RAS_STAMP(3);
   raster_env<NT, FLOW, FMT, true>(cfg, e, 0, cfg.grid * cfg.grid, st.record, ob.state_m, sm_stride, sm_frame, newest_only,
                        ob.potential, ob.flow, tile_log2r, s_ecur, s_eprev, s_vel, s_hdr);
+#ifdef FFMP_TRACE
+  __syncthreads();
+  FFMP_RAS_STAMP(2);
+#endif
 }
 
 // ============================================================================

@@ -18,12 +18,13 @@ from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+fused = len(sys.argv) > 3 and sys.argv[3] == "fused"
 lib = _abi.load()
 lib.ffmp_trace_read.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 env_t = np.zeros((4096, 12), np.uint64)
 ras_t = np.zeros((65536, 4), np.uint64)
 
-env = FFMPVec(n, preset(name), device="cuda:0", fused=False)
+env = FFMPVec(n, preset(name), device="cuda:0", fused=fused)
 env.reset()
 acts = torch.randint(0, 28, (40, n), device="cuda:0")
 for k in range(30):
@@ -31,6 +32,21 @@ for k in range(30):
 torch.cuda.synchronize()
 lib.ffmp_trace_read(env_t.ctypes.data, ras_t.ctypes.data, 1)
 print(f"{name} n={n} shape={env.raster_shape_newest if hasattr(env, 'raster_shape_newest') else '?'}", flush=True)
+if fused:  # one block per env: env step (wave 0) then the block's raster; stamps 0 / 3 / 2
+    for rep in range(3):
+        env.step(acts[30 + rep])
+        torch.cuda.synchronize()
+        lib.ffmp_trace_read(env_t.ctypes.data, ras_t.ctypes.data, 1)
+        R = ras_t[:min(n, 65536)].astype(np.int64)
+        r0 = R[:, 0].min()
+        us = lambda a: a * 0.01
+        envp, rasp, tot = R[:, 3] - R[:, 0], R[:, 2] - R[:, 3], R[:, 2] - R[:, 0]
+        print(f"-- fused step {rep}: span {us(R[:, 2].max() - r0):.1f} us, {len(R)} blocks")
+        for nm, d in (("env phase", envp), ("raster phase", rasp), ("block", tot)):
+            print(f"   {nm:14s} median {us(np.median(d)):7.2f}  p10 {us(np.percentile(d, 10)):7.2f}  "
+                  f"p90 {us(np.percentile(d, 90)):7.2f}  max {us(d.max()):7.2f} us")
+        print(f"   env-phase share of block time: {envp.sum() / tot.sum():.3f}")
+    sys.exit(0)
 for rep in range(3):
     env.step(acts[30 + rep])
     torch.cuda.synchronize()

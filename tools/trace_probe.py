@@ -46,6 +46,15 @@ if fused:  # one block per env: env step (wave 0) then the block's raster; stamp
             print(f"   {nm:14s} median {us(np.median(d)):7.2f}  p10 {us(np.percentile(d, 10)):7.2f}  "
                   f"p90 {us(np.percentile(d, 90)):7.2f}  max {us(d.max()):7.2f} us")
         print(f"   env-phase share of block time: {envp.sum() / tot.sum():.3f}")
+        E = env_t[:min(n, 4096)].astype(np.int64)
+        names = ["load+integrate", "lidar_disc+cos/sin+ego", "collide+lidar+reward", "reset", "grad+record",
+                 "writes"]
+        for k in range(6):
+            d = E[:, k + 1] - E[:, k]
+            print(f"   env {names[k]:24s} median {us(np.median(d)):6.2f}  p90 {us(np.percentile(d, 90)):6.2f} us")
+        for a, b, nm in ((2, 7, "  footprint"), (7, 8, "  lidar scene + beams"), (8, 9, "  ballots, reward, state_g")):
+            d = E[:, b] - E[:, a]
+            print(f"   env {nm:24s} median {us(np.median(d)):6.2f}  p90 {us(np.percentile(d, 90)):6.2f} us")
     sys.exit(0)
 for rep in range(3):
     env.step(acts[30 + rep])

@@ -139,12 +139,13 @@ class FFMPVec:
         plane_bytes = self.num_envs * G2 * (2 * self._fes + (self._pes if potential else 0) +
                                             (8 if self.cfg.flow else 0))
         paired = self.ring == "seamless" and self.with_potential
-        if paired and plane_bytes >= self.REPLACE_MIN_BYTES and (tuning is not None or autotune):
-            self._relocate_partner()
+        if paired and plane_bytes >= self.RELOCATE_MIN_BYTES and (tuning is not None or autotune):
+            self._relocate_partner(self.PARTNER_TRIES if plane_bytes >= self.REPLACE_MIN_BYTES
+                                   else self.PARTNER_TRIES_SMALL)
         self._build_structs()
         if tuning is not None:
             self._apply_tuning(tuning)
-            if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
+            if paired and plane_bytes >= self.RELOCATE_MIN_BYTES:
                 self._repair_slots()
                 self.placement = dict(self.placement, ring=self.ring_meta)
         elif autotune and plane_bytes >= self.AUTOTUNE_MIN_BYTES:
@@ -153,7 +154,7 @@ class FFMPVec:
             # would undo that
             if self.arena and plane_bytes >= self.REPLACE_MIN_BYTES and not paired:
                 self._retry_placement()
-            if paired and plane_bytes >= self.REPLACE_MIN_BYTES:
+            if paired and plane_bytes >= self.RELOCATE_MIN_BYTES:
                 self._repair_slots()
             if self.placement is not None and self.ring_meta is not None:
                 self.placement = dict(self.placement, ring=self.ring_meta)
@@ -420,10 +421,16 @@ class FFMPVec:
     # the allocator must return different memory — and a ring is paired against the new plane
     # (the losing rings' pieces return to the pool and are probed again first); the pair with the
     # fastest probe is kept.
+    # Small planes too (round 2, profiles/r02_env_chain.txt): at C2 (0.5 GB of planes, 256-MiB
+    # ring pieces) every first probe paired at 5.3-5.6 TB/s and the raster ran 0.106 ms; the third
+    # relocation found a 6.8 TB/s pair on each of three fresh runs, raster 0.089 ms (+16 % env-steps/s).
+    # Below REPLACE_MIN_BYTES a try is cheap (a < 4 GiB arena, a few 256-MiB probes), so more are allowed.
     PAIR_FAST_GBS = 6200.0  # ffmp_ring.hip kPairFastGBs
     PARTNER_TRIES = 3
+    PARTNER_TRIES_SMALL = 6
+    RELOCATE_MIN_BYTES = 512 << 20  # planes of C2 size up (the ring pairs pieces of >= 256 MiB)
 
-    def _relocate_partner(self) -> None:
+    def _relocate_partner(self, max_tries: int) -> None:
         meta = self.ring_meta or {}
         if not meta.get("pair_probes") or meta.get("pair_gbs_max", 0.0) >= self.PAIR_FAST_GBS:
             return
@@ -436,7 +443,7 @@ class FFMPVec:
         best = snap()
         tries, held = [best["gbs"]], []
         ring_bytes = self.frame_window * self._ring.slot_stride
-        for k in range(self.PARTNER_TRIES):
+        for k in range(max_tries):
             free, _ = torch.cuda.mem_get_info(self.device)
             if free < self._arena_used + (k + 1) * self.PLACEMENT_SPACER + ring_bytes + (16 << 30):
                 break

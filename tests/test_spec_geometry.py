@@ -13,7 +13,9 @@ float64 from world coordinates, and apply it to the oracle (CPU) and to the HIP 
     rho = max(|c - o| - r, rho_min) < rho0, from world geometry (atol 2e-2 + rtol 1e-4: float32
     ego coordinates against a steep term near rho_min);
   * integrator — x' = x + v cos(yaw) dt, y' = y + v sin(yaw) dt, yaw' = wrap(yaw + w dt) with the
-    reference's literal command table, for envs that did not reset (1e-12).
+    reference's literal command table, for envs that did not reset (1e-12);
+  * obstacle motion — each coordinate advances by v dt or is mirrored off its wall |p| = W - r with
+    that velocity component negated; parked discs stay.
 """
 import math
 
@@ -152,13 +154,40 @@ def check_integrator(cfg, pose0, pose1, actions, reset):
     return [] if err.size == 0 or err.max() <= 1e-12 else [f"integrator off by {err.max():.3g}"]
 
 
+def check_obstacle_motion(cfg, obst0, obst1, orr, reset, tol=1e-12):
+    """Moving discs: each coordinate advances by v dt, or is mirrored off the wall |p| = W - r
+    (the overshoot folded back inside, that velocity component negated); speed is preserved;
+    parked discs (r = 0) and static configs stay put."""
+    bad = []
+    keep = ~np.asarray(reset)
+    W, dt = cfg.W, cfg.dt
+    for ax in (0, 1):
+        p0, v0, p1, v1 = obst0[..., ax], obst0[..., 2 + ax], obst1[..., ax], obst1[..., 2 + ax]
+        if not cfg.moving:
+            ok = (p1 == p0) & (v1 == v0)
+        else:
+            free = p0 + v0 * dt
+            lim = W - orr
+            mirrored = np.where(free > lim, 2 * lim - free, np.where(free < -lim, -2 * lim - free, free))
+            flipped = np.where((free > lim) | (free < -lim), -v0, v0)
+            moving = orr > 0
+            ok = np.where(moving, (np.abs(p1 - mirrored) <= tol) & (v1 == flipped) & (np.abs(p1) <= lim + tol),
+                          (p1 == p0) & (v1 == v0))
+        if not np.all(ok[keep]):
+            e, k = np.argwhere(~ok & keep[:, None])[0]
+            bad.append(f"env {e} disc {k} axis {ax}: {p0[e, k]} + {v0[e, k]} dt -> {p1[e, k]}, v {v1[e, k]}")
+    return bad
+
+
 CFG = FFMPConfig(grid=64, n_obst=12, n_beams=90, moving=True, obst_rmax=0.5, obst_vmax=1.0, world_half=2.4,
                  max_steps=8, seed=21)
 
 
-def _check_all(cfg, pose0, actions, pose1, goal, obst, obst_r, lidar, state_m, pot, done):
+def _check_all(cfg, pose0, actions, pose1, goal, obst, obst_r, lidar, state_m, pot, done, obst0=None):
     ox, oy = obst[..., 0], obst[..., 1]
     problems = check_integrator(cfg, pose0, pose1, actions, done)
+    if obst0 is not None:
+        problems += check_obstacle_motion(cfg, obst0, obst, obst_r, done)
     problems += check_lidar(cfg, pose1, ox, oy, obst_r, lidar)
     problems += check_occupancy(cfg, pose1, ox, oy, obst_r, state_m[:, 1])
     problems += check_potential(cfg, pose1, goal, ox, oy, obst_r, pot)
@@ -174,10 +203,10 @@ def test_spec_geometry_oracle():
     hits = finite = resets = 0
     for _ in range(10):
         a = rng.integers(0, 28, n)
-        pose0 = env.pose.copy()
+        pose0, obst0 = env.pose.copy(), env.obst.copy()
         env.step(a)
         problems = _check_all(CFG, pose0, a, env.pose, env.goal, env.obst, env.obst_r, env.lidar, env.state_m,
-                              env.potential, env.done)
+                              env.potential, env.done, obst0)
         assert not problems, "\n".join(problems[:10])
         hits += int((env.state_m[:, 1] != 0).sum())
         finite += int(np.isfinite(env.lidar).sum())
@@ -197,12 +226,12 @@ def test_spec_geometry_hip(cfg, n):
     acts = torch.randint(0, 28, (8, n), device="cuda:0", generator=gen)
     finite = 0
     for k in range(8):
-        pose0 = env.pose.cpu().numpy()
+        pose0, obst0 = env.pose.cpu().numpy(), env.obst.cpu().numpy()
         obs, _, done, _ = env.step(acts[k])
         torch.cuda.synchronize()
         problems = _check_all(cfg, pose0, acts[k].cpu().numpy(), env.pose.cpu().numpy(), env.goal.cpu().numpy(),
                               env.obst.cpu().numpy(), env.obst_r.cpu().numpy(), obs["lidar"].cpu().numpy(),
-                              obs["state_m"].cpu().numpy(), obs["potential"].cpu().numpy(), done.cpu().numpy())
+                              obs["state_m"].cpu().numpy(), obs["potential"].cpu().numpy(), done.cpu().numpy(), obst0)
         assert not problems, "\n".join(problems[:10])
         finite += int(torch.isfinite(obs["lidar"]).sum())
     assert finite > 0

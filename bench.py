@@ -42,9 +42,8 @@ def parse():
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--flow", action="store_true", help="also raster the BEV motion-flow planes (not a BASELINE config)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
-    p.add_argument("--cpu-procs", type=int, default=16,
-                   help="processes of the parallel CPU baseline (SURVEY 8d (ii); capped at the host's CPUs, 0 = skip)")
-    p.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="host threads of the C-oracle CPU baseline (SURVEY 8d (ii); capped at the host's CPUs)")
     p.add_argument("--dump-launches", action="store_true", help="print every timed raster launch (ms) to stderr")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
@@ -69,72 +68,41 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(cfg, seconds: float):
-    """The NumPy oracle (oracle/ffmp_oracle.py) stepping a bounded sample of the same workload."""
+def _time_oracle(env, n, seconds: float, seed: int):
+    """Step an oracle env on random actions for about `seconds`; (env-steps, seconds)."""
     import numpy as np
-    from oracle.ffmp_oracle import OracleVecEnv
-    n = 4
-    env = OracleVecEnv(cfg, n)
+    rng = np.random.default_rng(seed)
     env.reset()
-    rng = np.random.default_rng(0)
     env.step(rng.integers(0, 28, n))  # warm
-    steps = 0
-    t0 = time.perf_counter()
+    steps, t0 = 0, time.perf_counter()
     while True:
         env.step(rng.integers(0, 28, n))
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": n * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} envs x {steps} steps of the same config ({el:.1f} s), NumPy oracle "
-                      f"OracleVecEnv, 1 process / 1 thread"}
+            return n * steps, el
 
 
-def cpu_worker(spec: str) -> None:
-    """Child of the parallel CPU baseline: one oracle shard for `seconds`, prints its count."""
-    import numpy as np
-    from flow_field_based_motion_planner_amd.config import FFMPConfig
+def cpu_baseline(cfg, seconds: float, threads: int):
+    """The C restatement of the oracle (oracle/ffmp_oracle.c, bit-identical to the NumPy oracle:
+    tests/test_oracle_c.py) stepping a bounded sample of the same workload on `threads` host
+    threads (one env per thread at a time, OpenMP over envs) — SURVEY 8(d)(ii) — plus the same on
+    one thread (8(d)(i)) and the NumPy oracle on one thread (the round-1 baseline)."""
     from oracle.ffmp_oracle import OracleVecEnv
-    d = json.loads(spec)
-    cfg = FFMPConfig(**d["cfg"])
-    n = d["envs"]
-    env = OracleVecEnv(cfg, n, env_offset=d["offset"])
-    env.reset()
-    rng = np.random.default_rng(d["offset"])
-    env.step(rng.integers(0, 28, n))
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < d["seconds"]:
-        env.step(rng.integers(0, 28, n))
-        steps += 1
-    print(json.dumps({"env_steps": n * steps, "seconds": time.perf_counter() - t0}), flush=True)
-
-
-def cpu_baseline_parallel(cfg, seconds: float, procs: int):
-    """`procs` single-threaded processes, one oracle shard of 4 envs each, run
-    concurrently as child processes; aggregate env-steps/s."""
-    import subprocess
-    procs = max(1, min(procs, os.cpu_count() or 1))
-    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
-               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
-    kids = []
-    for r in range(procs):
-        spec = json.dumps({"cfg": cfg.to_dict(), "envs": 4, "offset": 4 * r, "seconds": seconds})
-        kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", spec],
-                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, text=True))
-    rate, done = 0.0, 0
-    for k in kids:
-        out, _ = k.communicate(timeout=seconds * 4 + 120)
-        lines = [l for l in out.splitlines() if l.startswith("{")]
-        if k.returncode == 0 and lines:
-            d = json.loads(lines[-1])
-            rate += d["env_steps"] / d["seconds"]
-            done += 1
-    if done != procs:
-        return None
-    return {"value": rate, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x 4 envs of the same config, {seconds:.0f} s each, NumPy oracle, "
-                      f"1 thread per process"}
+    from oracle.ffmp_oracle_c import COracleVecEnv, load
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    # single-threaded legs first: the OpenMP pool's idle threads spin for a while after a region
+    k2, el2 = _time_oracle(OracleVecEnv(cfg, 4), 4, seconds / 3, 2)
+    k1, el1 = _time_oracle(COracleVecEnv(cfg, 4, threads=1), 4, seconds / 3, 1)
+    n = 4 * threads
+    k, el = _time_oracle(COracleVecEnv(cfg, n, threads=threads), n, seconds, 0)
+    return {"value": k / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {k // n} steps of the same config ({el:.1f} s), C oracle "
+                      f"(oracle/ffmp_oracle.c, {os.path.basename(load().path)}), {threads} threads",
+            "one_core": {"value": k1 / el1, "cores": 1, "sample": f"4 envs x {k1 // 4} steps ({el1:.1f} s), 1 thread"},
+            "numpy_one_core": {"value": k2 / el2, "cores": 1,
+                               "sample": f"4 envs x {k2 // 4} steps ({el2:.1f} s), NumPy oracle OracleVecEnv, "
+                                         f"1 thread"}}
 
 
 def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):
@@ -200,9 +168,6 @@ def time_compact(FFMPVec, name, cfg, n, dev, steps, warmup, seed):
 
 def main():
     args = parse()
-    if args.cpu_worker is not None:
-        cpu_worker(args.cpu_worker)
-        return
     import torch
     import torch.distributed as dist
     from flow_field_based_motion_planner_amd.config import PRESETS, bytes_per_env_step, preset
@@ -340,9 +305,7 @@ def main():
         if compact is not None:
             out["compact_layout"] = compact
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-            if args.cpu_procs > 0:
-                out["cpu_baseline_parallel"] = cpu_baseline_parallel(cfg, min(args.cpu_seconds, 10.0), args.cpu_procs)
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -57,3 +57,31 @@ def test_hip_equals_c_oracle(name):
     assert events["trunc"] > 0, events
     if name == "crowded_4096":
         assert events["collision"] > 0 and events["goal"] > 0 and events["inside"] > 0, events
+
+
+def test_full_c3_batch_bit_exact():
+    """The metric's whole workload — 32,768 envs of C3 on the production path (autotuned launch
+    shapes, seamless frame ring, one- or two-launch step as the autotune picks) — against the C
+    oracle, every env, compared in 4,096-env slices: reset and two steps (the second
+    truncates and auto-resets every env: max_steps = 2)."""
+    cfg = preset("C3", max_steps=2, seed=31)
+    n = 32768
+    env = FFMPVec(n, cfg, device="cuda:0")
+    ref = COracleVecEnv(cfg, n, threads=16)
+    env.reset()
+    ref.reset()
+    rng = np.random.default_rng(8)
+    for s in range(3):
+        if s:
+            a = rng.integers(0, 28, n)
+            env.step(torch.as_tensor(a, device="cuda:0"))
+            ref.step(a)
+        torch.cuda.synchronize()
+        problems = []
+        for e0 in range(0, n, 4096):
+            sl = slice(e0, e0 + 4096)
+            o = oracle_snapshot(ref)
+            o = {k: (None if v is None else v[sl]) for k, v in o.items()}
+            problems += compare(gpu_snapshot(env, sl), o, f"step {s} envs {e0}+")
+            assert not problems, "\n".join(problems[:20])
+    assert int(env.episode.sum()) > 0  # the auto-reset path ran

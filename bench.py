@@ -96,13 +96,30 @@ def cpu_baseline(cfg, seconds: float, threads: int):
     k1, el1 = _time_oracle(COracleVecEnv(cfg, 4, threads=1), 4, seconds / 3, 1)
     n = 4 * threads
     k, el = _time_oracle(COracleVecEnv(cfg, n, threads=threads), n, seconds, 0)
-    return {"value": k / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    from flow_field_based_motion_planner_amd.config import preset
+    c1 = preset("C1")  # BASELINE configs[0]: one env, 64x64, 4 static discs, the reference's CPU case
+    k3, el3 = _time_oracle(OracleVecEnv(c1, 1), 1, 2.0, 3)
+    return {"value": k / el, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": _cpu_model(),
             "sample": f"{n} envs x {k // n} steps of the same config ({el:.1f} s), C oracle "
                       f"(oracle/ffmp_oracle.c, {os.path.basename(load().path)}), {threads} threads",
             "one_core": {"value": k1 / el1, "cores": 1, "sample": f"4 envs x {k1 // 4} steps ({el1:.1f} s), 1 thread"},
             "numpy_one_core": {"value": k2 / el2, "cores": 1,
                                "sample": f"4 envs x {k2 // 4} steps ({el2:.1f} s), NumPy oracle OracleVecEnv, "
-                                         f"1 thread"}}
+                                         f"1 thread"},
+            "c1_numpy_single_env": {"value": k3 / el3, "cores": 1,
+                                    "sample": f"C1 (1 env, 64x64, 4 static discs, no lidar): {k3} steps "
+                                              f"({el3:.1f} s), NumPy oracle, 1 thread"}}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):

@@ -13,6 +13,11 @@ are re-rastered there, and the Q-networks run on the batch without host round tr
       Q_main(s',a), y = r + GAMMA * Q_target(s', a*) (no terminal mask, as the reference;
       mask_terminal=True multiplies by 1 - done), MSE, Adam step
   Brain.update_target_q_network (:430-431)      -> same
+
+amp=True (not the reference's arithmetic, opt-in): the Q-network forwards (acting, replay and
+target) run under torch.autocast bfloat16 — the convolutions on the MFMA units in bf16, fp32
+accumulation, fp32 master weights, Adam state and loss (tests/test_gpu_learner.py bounds the
+difference to the fp32 update).
 """
 from __future__ import annotations
 
@@ -35,12 +40,13 @@ INPUT_CHANNELS = 2      # train.py:68
 class Brain:
     def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
                  lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
-                 seed: int = 0):
+                 seed: int = 0, amp: bool = False):
         self.env = env
         self.device = env.device
         self.num_actions = NUM_ACTIONS
         self.batch_size, self.gamma, self.mask_terminal = int(batch_size), float(gamma), bool(mask_terminal)
         self.replay_coupling = replay_coupling
+        self.amp = bool(amp)
         self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed)
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
@@ -53,13 +59,13 @@ class Brain:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed) + 1)
 
-    @staticmethod
-    def _q(net: Network, coupling: str, sm, sg, sv, st):
+    def _q(self, net: Network, coupling: str, sm, sg, sv, st):
         prev, net.coupling = net.coupling, coupling
         if sm.dtype == torch.uint8:  # FFMPVec(obs_format="u8f16"): the same 0/255 values, as float
             sm = sm.float()
         try:
-            return net(sm, sg, sv, st)
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=self.amp):
+                return net(sm, sg, sv, st).float()
         finally:
             net.coupling = prev
 

@@ -86,3 +86,26 @@ def test_decide_action_epsilon_greedy():
     first = brain.decide_action(obs, torch.zeros(256, dtype=torch.int32, device=DEV))  # epsilon 0.5
     frac = float((first != greedy).float().mean())
     assert 0.3 < frac < 0.65 and first.dtype == torch.int64 and int(first.max()) < 28
+
+
+def test_amp_update_close_to_fp32():
+    """Brain(amp=True): the same update with the Q-network forwards in bfloat16 autocast — loss
+    within bf16 rounding of the fp32 update's on the same minibatch and weights, every parameter
+    moved by Adam (fp32 master weights), valid greedy actions."""
+    env = _env()
+    b32 = Brain(env, capacity=256, batch_size=48, seed=3)
+    b16 = Brain(env, capacity=256, batch_size=48, seed=3, amp=True)
+    b16.memory = b32.memory
+    _fill(b32, env, 3)
+    idx = torch.randperm(len(b32.memory), device=DEV)[:48]
+    before = [p.detach().clone() for p in b16.main_q_network.parameters()]
+    l32 = b32.replay(index=idx)
+    l16 = b16.replay(index=idx)
+    assert torch.isfinite(l16) and l16.dtype == torch.float32
+    torch.testing.assert_close(l16, l32, rtol=5e-2, atol=5e-3)
+    for p, q in zip(b16.main_q_network.parameters(), before):
+        assert p.dtype == torch.float32 and not torch.equal(p, q)
+    obs = env.obs
+    a32 = b32.decide_action(obs, torch.full((env.num_envs,), 10 ** 9, device=DEV))
+    a16 = b16.decide_action(obs, torch.full((env.num_envs,), 10 ** 9, device=DEV))
+    assert a16.dtype == torch.int64 and int(a16.max()) < 28

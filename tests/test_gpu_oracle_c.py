@@ -85,3 +85,32 @@ def test_full_c3_batch_bit_exact():
             problems += compare(gpu_snapshot(env, sl), o, f"step {s} envs {e0}+")
             assert not problems, "\n".join(problems[:20])
     assert int(env.episode.sum()) > 0  # the auto-reset path ran
+
+
+@pytest.mark.parametrize("name,n,sl", [("C5", 16384, 512), ("C4", 65536, 2048)])
+def test_whole_share_in_slices(name, n, sl):
+    """The C5 per-GPU share (16,384 envs of 512^2, 32 discs, 360 beams: the HBM stress config) and
+    all of C4 (65,536 envs of 256^2) on one GPU, checked in env slices: envs are independent and
+    every draw is keyed by the global env index, so a C oracle holding only envs [e0, e0 + sl)
+    (env_offset = e0) and fed those envs' actions steps exactly those envs.  Three slices spread
+    over the batch (first, middle, last), reset and two steps (the second truncates and resets
+    every env); contiguous (N,2,G,G) frames, so the full-launch raster is the one checked here."""
+    cfg = preset(name, max_steps=2, seed=41)
+    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False)
+    starts = [0, (n // 2 // sl) * sl + 7, n - sl]
+    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
+    env.reset()
+    for r in refs:
+        r.reset()
+    rng = np.random.default_rng(9)
+    for s in range(3):
+        if s:
+            a = rng.integers(0, 28, n)
+            env.step(torch.as_tensor(a, device="cuda:0"))
+            for e0, r in zip(starts, refs):
+                r.step(a[e0:e0 + sl])
+        torch.cuda.synchronize()
+        for e0, r in zip(starts, refs):
+            problems = compare(gpu_snapshot(env, slice(e0, e0 + sl)), oracle_snapshot(r), f"{name} step {s} envs {e0}+")
+            assert not problems, "\n".join(problems[:20])
+    assert int(env.truncated.sum()) == n  # max_steps = 2: the second step ended every episode

@@ -85,6 +85,7 @@ def test_full_c3_batch_bit_exact():
             problems += compare(gpu_snapshot(env, sl), o, f"step {s} envs {e0}+")
             assert not problems, "\n".join(problems[:20])
     assert int(env.episode.sum()) > 0  # the auto-reset path ran
+    env.close()  # hand the 80 GB back before the next whole-batch case
 
 
 @pytest.mark.parametrize("name,n,sl", [("C5", 16384, 512), ("C4", 65536, 2048)])
@@ -114,3 +115,39 @@ def test_whole_share_in_slices(name, n, sl):
             problems = compare(gpu_snapshot(env, slice(e0, e0 + sl)), oracle_snapshot(r), f"{name} step {s} envs {e0}+")
             assert not problems, "\n".join(problems[:20])
     assert int(env.truncated.sum()) == n  # max_steps = 2: the second step ended every episode
+    env.close()
+
+
+def test_compact_c5_whole_on_one_gpu_in_slices():
+    """All 131,072 envs of C5 on ONE GPU in the compact layout (uint8 frames, binary16 potential:
+    137 GB of planes; its raster goes out as several launches, > 2^31 work-items), checked in env
+    slices against C oracles holding only those envs: frames == the f32 oracle frames as uint8,
+    potential == the f32 oracle potential rounded to binary16, the rest as tests/parity_util.py
+    (records, flags, counters bit-exact)."""
+    cfg = preset("C5", max_steps=2, seed=43)
+    n, sl = 131072, 384
+    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False, obs_format="u8f16")
+    starts = [0, 65536 + 5, n - sl]
+    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
+    env.reset()
+    for r in refs:
+        r.reset()
+    rng = np.random.default_rng(10)
+    for s in range(3):
+        if s:
+            a = rng.integers(0, 28, n)
+            env.step(torch.as_tensor(a, device="cuda:0"))
+            for e0, r in zip(starts, refs):
+                r.step(a[e0:e0 + sl])
+        torch.cuda.synchronize()
+        for e0, r in zip(starts, refs):
+            w = slice(e0, e0 + sl)
+            tag = f"step {s} envs {e0}+"
+            g = gpu_snapshot(env, w)
+            assert g["state_m"].dtype == np.uint8 and g["potential"].dtype == np.float16
+            assert np.array_equal(g["potential"].view(np.uint16), r.potential.astype(np.float16).view(np.uint16)), tag
+            g["state_m"] = g["state_m"].astype(np.float32)  # 0 / 255, compared exactly below
+            g["potential"] = None
+            problems = compare(g, oracle_snapshot(r), tag)
+            assert not problems, "\n".join(problems[:20])
+    env.close()

@@ -3,6 +3,8 @@ oracle, tests/test_oracle_c.py) at whole-config batch sizes the NumPy oracle can
 seconds: all of C2 (4,096 envs), 2,048 envs of the C3 geometry through both step kinds, a crowded
 batch with collisions / goals / sensors inside discs, and the C5 geometry.  Same tolerances as
 tests/test_gpu_parity.py (tests/parity_util.py): planes, flags, counters and records bit-exact."""
+import warnings
+
 import numpy as np
 import pytest
 import torch
@@ -24,6 +26,78 @@ CASES = {
                                 max_steps=6, seed=24), 4096, 10, None),
     "C5_geometry_48": (preset("C5", max_steps=3, seed=25), 48, 4, None),
 }
+
+
+def test_compact_c5_whole_on_one_gpu_in_slices():
+    """All 131,072 envs of C5 on ONE GPU in the compact layout (uint8 frames, binary16 potential:
+    137 GB of planes; its raster goes out as several launches, > 2^31 work-items), checked in env
+    slices against C oracles holding only those envs: frames == the f32 oracle frames as uint8,
+    potential == the f32 oracle potential rounded to binary16, the rest as tests/parity_util.py
+    (records, flags, counters bit-exact)."""
+    cfg = preset("C5", max_steps=2, seed=43)
+    sl = 384
+    # first in this file (before the seamless rings of the later cases are parked in the process's
+    # piece pool); a box whose HBM is already held elsewhere runs half the workload
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    n = 131072 if free > 131072 * 512 * 512 * 3 * 1.05 + (8 << 30) else 65536
+    if n < 131072:
+        warnings.warn(f"only {free / 2**30:.0f} GiB of HBM free: half the C5 workload checked")
+    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False, obs_format="u8f16")
+    starts = [0, n // 2 + 5, n - sl]
+    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
+    env.reset()
+    for r in refs:
+        r.reset()
+    rng = np.random.default_rng(10)
+    for s in range(3):
+        if s:
+            a = rng.integers(0, 28, n)
+            env.step(torch.as_tensor(a, device="cuda:0"))
+            for e0, r in zip(starts, refs):
+                r.step(a[e0:e0 + sl])
+        torch.cuda.synchronize()
+        for e0, r in zip(starts, refs):
+            w = slice(e0, e0 + sl)
+            tag = f"step {s} envs {e0}+"
+            g = gpu_snapshot(env, w)
+            assert g["state_m"].dtype == np.uint8 and g["potential"].dtype == np.float16
+            assert np.array_equal(g["potential"].view(np.uint16), r.potential.astype(np.float16).view(np.uint16)), tag
+            g["state_m"] = g["state_m"].astype(np.float32)  # 0 / 255, compared exactly below
+            g["potential"] = None
+            problems = compare(g, oracle_snapshot(r), tag)
+            assert not problems, "\n".join(problems[:20])
+    env.close()
+
+
+@pytest.mark.parametrize("name,n,sl", [("C5", 16384, 512), ("C4", 65536, 2048)])
+def test_whole_share_in_slices(name, n, sl):
+    """The C5 per-GPU share (16,384 envs of 512^2, 32 discs, 360 beams: the HBM stress config) and
+    all of C4 (65,536 envs of 256^2) on one GPU, checked in env slices: envs are independent and
+    every draw is keyed by the global env index, so a C oracle holding only envs [e0, e0 + sl)
+    (env_offset = e0) and fed those envs' actions steps exactly those envs.  Three slices spread
+    over the batch (first, middle, last), reset and two steps (the second truncates and resets
+    every env); contiguous (N,2,G,G) frames, so the full-launch raster is the one checked here."""
+    cfg = preset(name, max_steps=2, seed=41)
+    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False)
+    starts = [0, (n // 2 // sl) * sl + 7, n - sl]
+    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
+    env.reset()
+    for r in refs:
+        r.reset()
+    rng = np.random.default_rng(9)
+    for s in range(3):
+        if s:
+            a = rng.integers(0, 28, n)
+            env.step(torch.as_tensor(a, device="cuda:0"))
+            for e0, r in zip(starts, refs):
+                r.step(a[e0:e0 + sl])
+        torch.cuda.synchronize()
+        for e0, r in zip(starts, refs):
+            problems = compare(gpu_snapshot(env, slice(e0, e0 + sl)), oracle_snapshot(r), f"{name} step {s} envs {e0}+")
+            assert not problems, "\n".join(problems[:20])
+    assert int(env.truncated.sum()) == n  # max_steps = 2: the second step ended every episode
+    env.close()
 
 
 @pytest.mark.parametrize("name", list(CASES))
@@ -60,13 +134,16 @@ def test_hip_equals_c_oracle(name):
 
 
 def test_full_c3_batch_bit_exact():
-    """The metric's whole workload — 32,768 envs of C3 on the production path (autotuned launch
-    shapes, seamless frame ring, one- or two-launch step as the autotune picks) — against the C
-    oracle, every env, compared in 4,096-env slices: reset and two steps (the second
-    truncates and auto-resets every env: max_steps = 2)."""
+    """The metric's whole workload — 32,768 envs of C3 through the metric's one-launch step
+    (step_raster_kernel) — against the C oracle, every env, compared in 4,096-env slices: reset and
+    two steps (the second truncates and auto-resets every env: max_steps = 2).  Contiguous
+    (N,2,G,G) frames (full launches write both frames), so that no seamless ring's pieces stay
+    parked in the process for the later ring tests; the ring's newest-only launches are checked
+    bit-exact at 2,048 envs above and through properties at this size (test_gpu_parity.py)."""
     cfg = preset("C3", max_steps=2, seed=31)
     n = 32768
-    env = FFMPVec(n, cfg, device="cuda:0")
+    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, fused=True, autotune=False)
+    assert env.fused
     ref = COracleVecEnv(cfg, n, threads=16)
     env.reset()
     ref.reset()
@@ -86,68 +163,3 @@ def test_full_c3_batch_bit_exact():
             assert not problems, "\n".join(problems[:20])
     assert int(env.episode.sum()) > 0  # the auto-reset path ran
     env.close()  # hand the 80 GB back before the next whole-batch case
-
-
-@pytest.mark.parametrize("name,n,sl", [("C5", 16384, 512), ("C4", 65536, 2048)])
-def test_whole_share_in_slices(name, n, sl):
-    """The C5 per-GPU share (16,384 envs of 512^2, 32 discs, 360 beams: the HBM stress config) and
-    all of C4 (65,536 envs of 256^2) on one GPU, checked in env slices: envs are independent and
-    every draw is keyed by the global env index, so a C oracle holding only envs [e0, e0 + sl)
-    (env_offset = e0) and fed those envs' actions steps exactly those envs.  Three slices spread
-    over the batch (first, middle, last), reset and two steps (the second truncates and resets
-    every env); contiguous (N,2,G,G) frames, so the full-launch raster is the one checked here."""
-    cfg = preset(name, max_steps=2, seed=41)
-    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False)
-    starts = [0, (n // 2 // sl) * sl + 7, n - sl]
-    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
-    env.reset()
-    for r in refs:
-        r.reset()
-    rng = np.random.default_rng(9)
-    for s in range(3):
-        if s:
-            a = rng.integers(0, 28, n)
-            env.step(torch.as_tensor(a, device="cuda:0"))
-            for e0, r in zip(starts, refs):
-                r.step(a[e0:e0 + sl])
-        torch.cuda.synchronize()
-        for e0, r in zip(starts, refs):
-            problems = compare(gpu_snapshot(env, slice(e0, e0 + sl)), oracle_snapshot(r), f"{name} step {s} envs {e0}+")
-            assert not problems, "\n".join(problems[:20])
-    assert int(env.truncated.sum()) == n  # max_steps = 2: the second step ended every episode
-    env.close()
-
-
-def test_compact_c5_whole_on_one_gpu_in_slices():
-    """All 131,072 envs of C5 on ONE GPU in the compact layout (uint8 frames, binary16 potential:
-    137 GB of planes; its raster goes out as several launches, > 2^31 work-items), checked in env
-    slices against C oracles holding only those envs: frames == the f32 oracle frames as uint8,
-    potential == the f32 oracle potential rounded to binary16, the rest as tests/parity_util.py
-    (records, flags, counters bit-exact)."""
-    cfg = preset("C5", max_steps=2, seed=43)
-    n, sl = 131072, 384
-    env = FFMPVec(n, cfg, device="cuda:0", frame_window=2, autotune=False, obs_format="u8f16")
-    starts = [0, 65536 + 5, n - sl]
-    refs = [COracleVecEnv(cfg, sl, env_offset=e0, threads=16) for e0 in starts]
-    env.reset()
-    for r in refs:
-        r.reset()
-    rng = np.random.default_rng(10)
-    for s in range(3):
-        if s:
-            a = rng.integers(0, 28, n)
-            env.step(torch.as_tensor(a, device="cuda:0"))
-            for e0, r in zip(starts, refs):
-                r.step(a[e0:e0 + sl])
-        torch.cuda.synchronize()
-        for e0, r in zip(starts, refs):
-            w = slice(e0, e0 + sl)
-            tag = f"step {s} envs {e0}+"
-            g = gpu_snapshot(env, w)
-            assert g["state_m"].dtype == np.uint8 and g["potential"].dtype == np.float16
-            assert np.array_equal(g["potential"].view(np.uint16), r.potential.astype(np.float16).view(np.uint16)), tag
-            g["state_m"] = g["state_m"].astype(np.float32)  # 0 / 255, compared exactly below
-            g["potential"] = None
-            problems = compare(g, oracle_snapshot(r), tag)
-            assert not problems, "\n".join(problems[:20])
-    env.close()

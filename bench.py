@@ -93,9 +93,14 @@ def cpu_baseline(cfg, seconds: float, threads: int):
     threads = max(1, min(threads, os.cpu_count() or 1))
     # single-threaded legs first: the OpenMP pool's idle threads spin for a while after a region
     k2, el2 = _time_oracle(OracleVecEnv(cfg, 4), 4, seconds / 3, 2)
-    k1, el1 = _time_oracle(COracleVecEnv(cfg, 4, threads=1), 4, seconds / 3, 1)
-    n = 4 * threads
-    k, el = _time_oracle(COracleVecEnv(cfg, n, threads=threads), n, seconds, 0)
+    try:
+        k1, el1 = _time_oracle(COracleVecEnv(cfg, 4, threads=1), 4, seconds / 3, 1)
+        n = 4 * threads
+        k, el = _time_oracle(COracleVecEnv(cfg, n, threads=threads), n, seconds, 0)
+    except (OSError, RuntimeError) as exc:  # C oracle not built / not loadable here: the NumPy leg only
+        k3, el3 = _time_oracle(OracleVecEnv(cfg, 4), 4, seconds, 2)
+        return {"value": k3 / el3, "unit": "env-steps/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
+                "sample": f"4 envs x {k3 // 4} steps ({el3:.1f} s), NumPy oracle, 1 thread (C oracle unavailable: {exc})"}
     from flow_field_based_motion_planner_amd.config import preset
     c1 = preset("C1")  # BASELINE configs[0]: one env, 64x64, 4 static discs, the reference's CPU case
     k3, el3 = _time_oracle(OracleVecEnv(c1, 1), 1, 2.0, 3)

@@ -329,6 +329,11 @@ static void raster_env(const ffmpo_cfg* cfg, const ffmpo_env* v, int64_t e) {
   float* dyg = ey + G;
   float* dyy = ey + 2 * G;
   unsigned char* oc = (unsigned char*)malloc((size_t)G * 3);
+  if (!ey || !oc) {  /* out of host memory: leave the planes as they are (the checker then fails) */
+    free(ey);
+    free(oc);
+    return;
+  }
   unsigned char* op = oc + G;
   unsigned char* fdone = oc + 2 * G;
   for (int j = 0; j < G; ++j) {

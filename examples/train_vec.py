@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--obs-format", default="f32", choices=["f32", "u8f16"],
                     help="u8f16: uint8 state_m / float16 potential (the Brain converts on input)")
     ap.add_argument("--amp", action="store_true", help="Q-network forwards in bfloat16 autocast (Brain(amp=True))")
+    ap.add_argument("--channels-last", action="store_true", help="NHWC Q-networks (Brain(channels_last=True))")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
 
@@ -50,7 +51,8 @@ def main():
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed)
     env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format)
-    brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp)
+    brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
+                  channels_last=args.channels_last)
     obs = env.reset()
     tracker = EpisodeTracker(args.envs, device=dev)
     losses, updates = [], 0
@@ -80,7 +82,7 @@ def main():
     env.check_errors()
     summ = tracker.summary()
     out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "warmup_seconds": t_warm - t0,
-           "envs": args.envs, "steps": args.steps, "amp": args.amp,
+           "envs": args.envs, "steps": args.steps, "amp": args.amp, "channels_last": args.channels_last,
            "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],
            "replay_bytes": brain.memory.hbm_bytes(), "replay_len": len(brain.memory), **summ}
     print(json.dumps(out))

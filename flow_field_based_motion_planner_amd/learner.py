@@ -40,19 +40,23 @@ INPUT_CHANNELS = 2      # train.py:68
 class Brain:
     def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
                  lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
-                 seed: int = 0, amp: bool = False):
+                 seed: int = 0, amp: bool = False, channels_last: bool = False):
         self.env = env
         self.device = env.device
         self.num_actions = NUM_ACTIONS
         self.batch_size, self.gamma, self.mask_terminal = int(batch_size), float(gamma), bool(mask_terminal)
         self.replay_coupling = replay_coupling
         self.amp = bool(amp)
+        self.channels_last = bool(channels_last)
         self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed)
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
             torch.manual_seed(seed)
             self.main_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
             self.target_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
+        if self.channels_last:  # NHWC convolutions (same values; MIOpen picks other kernels)
+            self.main_q_network.to(memory_format=torch.channels_last)
+            self.target_q_network.to(memory_format=torch.channels_last)
         self.optimizer = torch.optim.Adam(self.main_q_network.parameters(), lr=lr)
         self.loss: Optional[torch.Tensor] = None
         self.step = 0
@@ -63,6 +67,8 @@ class Brain:
         prev, net.coupling = net.coupling, coupling
         if sm.dtype == torch.uint8:  # FFMPVec(obs_format="u8f16"): the same 0/255 values, as float
             sm = sm.float()
+        if self.channels_last:
+            sm = sm.contiguous(memory_format=torch.channels_last)
         try:
             with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=self.amp):
                 return net(sm, sg, sv, st).float()

@@ -26,7 +26,7 @@ from typing import Dict, Optional
 import torch
 import torch.nn as nn
 
-from .network import Network
+from .network import Network, map_channels
 from .replay import ReplayMemory
 
 GAMMA = 0.95            # train.py:57
@@ -40,7 +40,8 @@ INPUT_CHANNELS = 2      # train.py:68
 class Brain:
     def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
                  lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
-                 seed: int = 0, amp: bool = False, channels_last: bool = False):
+                 seed: int = 0, amp: bool = False, channels_last: bool = False,
+                 input_channels: int = INPUT_CHANNELS):
         self.env = env
         self.device = env.device
         self.num_actions = NUM_ACTIONS
@@ -48,12 +49,19 @@ class Brain:
         self.replay_coupling = replay_coupling
         self.amp = bool(amp)
         self.channels_last = bool(channels_last)
+        # map input per train.py:66-69 (network.map_channels): 2 = [older, newest] (default), 1 =
+        # newest frame, 3 = newest frame + flow xy (needs the env's flow planes)
+        self.input_channels = int(input_channels)
+        if self.input_channels == 3 and not env.cfg.flow:
+            raise ValueError("input_channels=3 needs an env with FFMPConfig(flow=True)")
+        if self.input_channels not in (1, 2, 3):
+            raise ValueError("input_channels must be 1, 2 or 3")
         self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed)
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
             torch.manual_seed(seed)
-            self.main_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
-            self.target_q_network = Network(INPUT_CHANNELS, NUM_ACTIONS, grid=g).to(self.device)
+            self.main_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g).to(self.device)
+            self.target_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g).to(self.device)
         if self.channels_last:  # NHWC convolutions (same values; MIOpen picks other kernels)
             self.main_q_network.to(memory_format=torch.channels_last)
             self.target_q_network.to(memory_format=torch.channels_last)
@@ -63,12 +71,11 @@ class Brain:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed) + 1)
 
-    def _q(self, net: Network, coupling: str, sm, sg, sv, st):
-        prev, net.coupling = net.coupling, coupling
-        if sm.dtype == torch.uint8:  # FFMPVec(obs_format="u8f16"): the same 0/255 values, as float
-            sm = sm.float()
+    def _q(self, net: Network, coupling: str, sm, sg, sv, st, flow=None):
+        sm = map_channels(sm, flow, self.input_channels)  # uint8 frames (u8f16 layout) -> float 0 / 255
         if self.channels_last:
             sm = sm.contiguous(memory_format=torch.channels_last)
+        prev, net.coupling = net.coupling, coupling
         try:
             with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=self.amp):
                 return net(sm, sg, sv, st).float()
@@ -83,7 +90,7 @@ class Brain:
         self.main_q_network.eval()
         with torch.no_grad():
             q = self._q(self.main_q_network, "per_sample", obs["state_m"], obs["state_g"], obs["state_v"],
-                        obs["state_t"])
+                        obs["state_t"], obs.get("flow"))
         greedy = q.max(1)[1]
         rand = torch.randint(0, self.num_actions, (n,), generator=self.gen, device=self.device)
         return torch.where(epsilon <= u, greedy, rand)
@@ -96,11 +103,12 @@ class Brain:
         c = self.replay_coupling
         self.main_q_network.eval()
         self.target_q_network.eval()
-        sav = self._q(self.main_q_network, c, b.state_m, b.state_g, b.state_v, b.state_t).gather(1, b.action)
+        fs, fo = ex.get("flow"), ex.get("observe_flow")
+        sav = self._q(self.main_q_network, c, b.state_m, b.state_g, b.state_v, b.state_t, fs).gather(1, b.action)
         with torch.no_grad():
-            a_m = self._q(self.main_q_network, c, b.observe_m, b.observe_g, b.observe_v, b.observe_t).max(1)[1]
+            a_m = self._q(self.main_q_network, c, b.observe_m, b.observe_g, b.observe_v, b.observe_t, fo).max(1)[1]
             nxt = self._q(self.target_q_network, c, b.observe_m, b.observe_g, b.observe_v,
-                          b.observe_t).gather(1, a_m.view(-1, 1)).squeeze(1)
+                          b.observe_t, fo).gather(1, a_m.view(-1, 1)).squeeze(1)
             if self.mask_terminal:
                 nxt = nxt * (~ex["done"]).to(nxt.dtype)
             expected = b.reward + self.gamma * nxt

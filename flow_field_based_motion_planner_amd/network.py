@@ -66,3 +66,26 @@ class Network(nn.Module):
         adv = self.fc4_ea(x)
         val = self.fc4_ev(x)
         return adv + val - adv.mean(1, keepdim=True).expand(-1, adv.size(1))
+
+
+def map_channels(state_m: torch.Tensor, flow: "torch.Tensor | None", channels: int = 2) -> torch.Tensor:
+    """The map input of the reference's INPUT_CHANNELS options (src/train.py:66-69):
+      2  two steps of temporal_bev_image, [older, newest] — the configuration train.py runs (:69)
+      1  only temporal_bev_image: the newest frame (:68)
+      3  (occupancy(MONO) + flow(xy)) * series(1 steps) (:67): the newest frame, then the BEV
+         motion-flow planes (FFMPVec with cfg.flow: per-cell ego velocity of the covering disc)
+    (:66's 12 channels, occupancy + RGB flow over 3 steps, need an RGB encoding of the flow that the
+    reference's BEV nodes defined outside the repository: not offered.)  uint8 frames (the compact
+    layout) come back as float with the same 0 / 255 values."""
+    if state_m.dtype == torch.uint8:
+        state_m = state_m.float()
+    if channels == 2:
+        return state_m
+    if channels == 1:
+        return state_m[:, 1:2]
+    if channels == 3:
+        if flow is None:
+            raise ValueError("3 map channels need the flow planes (FFMPConfig(flow=True))")
+        return torch.cat((state_m[:, 1:2], flow), 1)
+    raise ValueError(f"map channels must be 1, 2 or 3 (train.py:66-69 without the RGB option), got {channels}")
+

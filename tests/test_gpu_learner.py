@@ -109,3 +109,34 @@ def test_amp_update_close_to_fp32():
     a32 = b32.decide_action(obs, torch.full((env.num_envs,), 10 ** 9, device=DEV))
     a16 = b16.decide_action(obs, torch.full((env.num_envs,), 10 ** 9, device=DEV))
     assert a16.dtype == torch.int64 and int(a16.max()) < 28
+
+
+@pytest.mark.parametrize("channels", [1, 3])
+def test_replay_with_other_input_channels(channels):
+    """Brain(input_channels=1 | 3): train.py:66-68's other map inputs (newest frame; newest frame +
+    flow xy from the env's flow planes, replayed from the records) — one update equals the restated
+    reference arithmetic on the same assembled inputs."""
+    from flow_field_based_motion_planner_amd.network import map_channels
+    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=64, moving=True, max_steps=6, seed=32, flow=channels == 3)
+    env = FFMPVec(32, cfg, device=DEV, keep_terminal=True)
+    env.reset()
+    brain = Brain(env, capacity=256, batch_size=40, seed=5, input_channels=channels)
+    assert brain.main_q_network.conv1.in_channels == channels
+    _fill(brain, env, 3)
+    idx = torch.randperm(len(brain.memory), device=DEV)[:40]
+    main0 = copy.deepcopy(brain.main_q_network)
+    targ0 = copy.deepcopy(brain.target_q_network)
+    b, ex = brain.memory.sample(40, index=idx)
+    s_in = map_channels(b.state_m, ex.get("flow"), channels).clone()
+    o_in = map_channels(b.observe_m, ex.get("observe_flow"), channels).clone()
+    b = type(b)(*[t.clone() for t in b])
+    loss = brain.replay(index=idx)
+    main0.eval()
+    targ0.eval()
+    sav = main0(s_in, b.state_g, b.state_v, b.state_t).gather(1, b.action)
+    a_m = main0(o_in, b.observe_g, b.observe_v, b.observe_t).detach().max(1)[1].view(-1, 1)
+    nxt = targ0(o_in, b.observe_g, b.observe_v, b.observe_t).gather(1, a_m).detach().squeeze()
+    ref_loss = nn.MSELoss()(sav, (b.reward + 0.95 * nxt).unsqueeze(1))
+    torch.testing.assert_close(loss, ref_loss.detach(), rtol=1e-5, atol=1e-5)
+    a = brain.decide_action(env.obs, torch.zeros(32, dtype=torch.int32, device=DEV))
+    assert a.shape == (32,) and int(a.max()) < 28

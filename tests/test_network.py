@@ -66,3 +66,23 @@ def test_grid_validation():
 @pytest.mark.gpu
 def test_reference_outputs_gpu(golden):
     _check(golden, "cuda:0", GPU_ATOL)
+
+
+def test_map_channels_options():
+    """train.py:66-69's INPUT_CHANNELS options: 2 = [older, newest], 1 = newest, 3 = newest + flow xy."""
+    import pytest
+    import torch
+
+    from flow_field_based_motion_planner_amd.network import map_channels
+    sm = torch.arange(2 * 2 * 4 * 4, dtype=torch.float32).reshape(2, 2, 4, 4)
+    fl = -torch.arange(2 * 2 * 4 * 4, dtype=torch.float32).reshape(2, 2, 4, 4)
+    assert map_channels(sm, None, 2) is sm
+    assert torch.equal(map_channels(sm, None, 1), sm[:, 1:2])
+    m3 = map_channels(sm, fl, 3)
+    assert m3.shape == (2, 3, 4, 4) and torch.equal(m3[:, 0], sm[:, 1]) and torch.equal(m3[:, 1:], fl)
+    u8 = (sm > 10).to(torch.uint8) * 255
+    assert map_channels(u8, None, 2).dtype == torch.float32 and torch.equal(map_channels(u8, None, 2), u8.float())
+    with pytest.raises(ValueError):
+        map_channels(sm, None, 3)
+    with pytest.raises(ValueError):
+        map_channels(sm, fl, 12)

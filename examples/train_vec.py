@@ -44,15 +44,18 @@ def main():
                     help="u8f16: uint8 state_m / float16 potential (the Brain converts on input)")
     ap.add_argument("--amp", action="store_true", help="Q-network forwards in bfloat16 autocast (Brain(amp=True))")
     ap.add_argument("--channels-last", action="store_true", help="NHWC Q-networks (Brain(channels_last=True))")
+    ap.add_argument("--input-channels", type=int, default=2, choices=[1, 2, 3],
+                    help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
 
     dev = torch.device("cuda:0")
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
-    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed)
+    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed,
+                     flow=args.input_channels == 3)
     env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
-                  channels_last=args.channels_last)
+                  channels_last=args.channels_last, input_channels=args.input_channels)
     obs = env.reset()
     tracker = EpisodeTracker(args.envs, device=dev)
     losses, updates = [], 0

@@ -202,14 +202,14 @@ def bytes_per_env_step(cfg: FFMPConfig, potential: bool = True, window: int = 2,
     plane (4 G^2) and, with cfg.flow, the two float32 flow planes (8 G^2); reads the raster
     record (64 + 48 K).  state kernel: reads/writes pose, goal, d0, t, episode, obstacles and
     writes the small obs, lidar and the record.  obs_format "u8f16" (FFMPVec): 1-byte frames and
-    a 2-byte potential plane instead.
+    a 2-byte potential plane (and 2-byte flow planes) instead.
     """
     G2 = cfg.grid * cfg.grid
     K, L = cfg.n_obst, cfg.n_beams
     rec = 4 * cfg.record_len()
     fb, pb = {"f32": (4, 4), "u8f16": (1, 2)}[obs_format]
     frames = fb * G2 + (0 if seamless and window > 2 else (fb * G2) // (max(int(window), 2) - 1))
-    raster = frames + (pb * G2 if potential else 0) + (8 * G2 if cfg.flow else 0) + rec
+    raster = frames + (pb * G2 if potential else 0) + (2 * pb * G2 if cfg.flow else 0) + rec
     state_rw = 2 * (24 + 16 + 8 + 4 + 4 + 40 * K)  # pose, goal, d0, t, episode, obst(32)+r(8)
     small_obs = 4 * (2 + 2 + 1 + 2) + 4 * L + rec + 8 + 4 + 4  # g, v, t, grad, lidar, record, action, reward, flags
     return {"raster": raster, "state": state_rw + small_obs, "total": raster + state_rw + small_obs}

@@ -82,7 +82,6 @@ int check_cfg(const ffmp_cfg_t* c) {
 int check_format(const ffmp_obs_t* o, bool flow) {
   if (o->format != FFMP_OBS_F32 && o->format != FFMP_OBS_U8F16)
     return fail(FFMP_E_ARG, "unknown obs.format %d", o->format);
-  if (o->format == FFMP_OBS_U8F16 && flow) return fail(FFMP_E_ARG, "obs.format U8F16 has no flow planes (cfg.flow)");
   return FFMP_OK;
 }
 
@@ -652,7 +651,8 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   uint8_t* b0 = CT ? reinterpret_cast<uint8_t*>(state_m) + e * sm_stride : nullptr;
   uint8_t* b1 = CT ? b0 + sm_frame : nullptr;
   _Float16* hp16 = (CT && pot) ? reinterpret_cast<_Float16*>(pot) + (int64_t)e * G2 : nullptr;
-  float* f0 = FLOW ? flow + (int64_t)e * 2 * G2 : nullptr;
+  float* f0 = (FLOW && !CT) ? flow + (int64_t)e * 2 * G2 : nullptr;
+  _Float16* h0 = (FLOW && CT) ? reinterpret_cast<_Float16*>(flow) + (int64_t)e * 2 * G2 : nullptr;  // binary16 flow
 
   const int qbeg = tile * cells_per_block;
   const int qend = min(qbeg + cells_per_block, G2);
@@ -723,12 +723,22 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
         store8_h<NT>(hp16 + q, U);
         store8_h<NT>(hp16 + q + 8, U + 8);
       }
+      if (FLOW) {
+        store8_h<NT>(h0 + q, fx);
+        store8_h<NT>(h0 + q + 8, fx + 8 % CPL);
+        store8_h<NT>(h0 + G2 + q, fy);
+        store8_h<NT>(h0 + G2 + q + 8, fy + 8 % CPL);
+      }
       return;
     }
     if (CT) {
       if (write_old) store4_u8<NT>(b0 + q, occp);
       store4_u8<NT>(b1 + q, occc);
       if (hp16) store4_h<NT>(hp16 + q, U[0], U[1], U[2], U[3]);
+      if (FLOW) {
+        store4_h<NT>(h0 + q, fx[0], fx[1], fx[2], fx[3]);
+        store4_h<NT>(h0 + G2 + q, fy[0], fy[1], fy[2], fy[3]);
+      }
       return;
     }
     if (write_old) store4<NT>(m0 + q, occp[0] * 255.0f, occp[1] * 255.0f, occp[2] * 255.0f, occp[3] * 255.0f);
@@ -862,6 +872,12 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
                 *reinterpret_cast<f16x8*>(hp16 + q + 8) = hi;
               }
             }
+            if (FLOW) {
+              store8_h<NT>(h0 + q, fx);
+              store8_h<NT>(h0 + q + 8, fx + 8 % CPL);
+              store8_h<NT>(h0 + G2 + q, fy);
+              store8_h<NT>(h0 + G2 + q + 8, fy + 8 % CPL);
+            }
           } else if (FMT == FMT_CT4) {
             if (NT) {
               if (write_old) __builtin_nontemporal_store(wp[0], reinterpret_cast<uint32_t*>(b0 + q));
@@ -871,6 +887,10 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
               *reinterpret_cast<uint32_t*>(b1 + q) = wc[0];
             }
             if (hp16) store4_h<NT>(hp16 + q, U2[0].x, U2[0].y, U2[NP - 1].x, U2[NP - 1].y);
+            if (FLOW) {
+              store4_h<NT>(h0 + q, fx[0], fx[1 % CPL], fx[2 % CPL], fx[3 % CPL]);
+              store4_h<NT>(h0 + G2 + q, fy[0], fy[1 % CPL], fy[2 % CPL], fy[3 % CPL]);
+            }
           } else {
             // byte 0xFF -> 255.0f, 0 -> 0.0f: the reference layout's occ * 255 values
             if (write_old)
@@ -1210,14 +1230,19 @@ int raster_format(bool compact, int grid, int32_t flags) {
 }
 
 // Calls f(NT, XCD, FLOW, FMT) with std::integral_constant arguments for the runtime choice (the
-// compact formats have no flow planes: check_format refused them before).
+// compact formats' flow planes are binary16).
 template <class F>
 void dispatch_variant(int fmt, bool nt, bool xcd, bool fl, F&& f) {
   using T = std::true_type;
   using N = std::false_type;
   auto with_fmt = [&](auto NT_, auto XCD_) {
-    if (fmt == FMT_CT16) f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT16>{});
-    else if (fmt == FMT_CT4) f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT4>{});
+    if (fmt == FMT_CT16) {
+      if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_CT16>{});
+      else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT16>{});
+    } else if (fmt == FMT_CT4) {
+      if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_CT4>{});
+      else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT4>{});
+    }
     else if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_F32>{});
     else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_F32>{});
   };
@@ -1407,7 +1432,7 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
     const uint8_t* msk = mask ? mask + e0 : nullptr;
     float* sm = (float*)((char*)obs->state_m + e0 * sm_stride * (ct ? 1 : 4));
     float* pot = obs->potential ? (float*)((char*)obs->potential + e0 * (int64_t)G2 * (ct ? 2 : 4)) : nullptr;
-    float* flw = obs->flow ? obs->flow + e0 * 2 * (int64_t)G2 : nullptr;
+    float* flw = obs->flow ? (float*)((char*)obs->flow + e0 * 2 * (int64_t)G2 * (ct ? 2 : 4)) : nullptr;
     dispatch_variant(fmt, nt, xcd, fl, [&](auto NT_, auto XCD_, auto FL_, auto FMT_) {
       hipLaunchKernelGGL((raster_kernel<decltype(NT_)::value, decltype(XCD_)::value, decltype(FL_)::value, decltype(FMT_)::value>), grid, block, tuning().lds_pad, s, *cfg, m,
                          bpe, cpb, rec, msk, sm, sm_stride, sm_frame, newest, pot, flw, tile_log2r);

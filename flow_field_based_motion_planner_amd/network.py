@@ -86,6 +86,6 @@ def map_channels(state_m: torch.Tensor, flow: "torch.Tensor | None", channels: i
     if channels == 3:
         if flow is None:
             raise ValueError("3 map channels need the flow planes (FFMPConfig(flow=True))")
-        return torch.cat((state_m[:, 1:2], flow), 1)
+        return torch.cat((state_m[:, 1:2], flow.float()), 1)  # binary16 flow (u8f16 layout) -> float
     raise ValueError(f"map channels must be 1, 2 or 3 (train.py:66-69 without the RGB option), got {channels}")
 

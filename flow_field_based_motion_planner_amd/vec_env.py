@@ -75,7 +75,7 @@ class FFMPVec:
             (include/ffmp.h FFMP_OBS_U8F16) for consumers that convert on load — state_m uint8
             with the same 0/255 values (`state_m.float()` is the f32 layout bit for bit) and the
             potential plane as float16 (the float32 value rounded to nearest even): 3 instead of
-            8 bytes per cell of a step's raster.  No flow planes.
+            8 bytes per cell of a step's raster.  With cfg.flow the flow planes are float16 too.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -102,8 +102,6 @@ class FFMPVec:
             raise ValueError("num_envs must be positive")
         if obs_format not in self.OBS_FORMATS:
             raise ValueError(f"obs_format must be one of {sorted(self.OBS_FORMATS)}, got {obs_format!r}")
-        if obs_format == "u8f16" and config.flow:
-            raise ValueError('obs_format="u8f16" has no flow planes (config.flow)')
         self.obs_format = obs_format
         self._fmt, self._frame_dtype, self._pot_dtype = self.OBS_FORMATS[obs_format]
         self._fes = torch.empty((), dtype=self._frame_dtype).element_size()  # bytes per frame cell
@@ -137,7 +135,7 @@ class FFMPVec:
         if self.pipeline_slices > 1:
             self._fused_req = False
         plane_bytes = self.num_envs * G2 * (2 * self._fes + (self._pes if potential else 0) +
-                                            (8 if self.cfg.flow else 0))
+                                            (2 * self._pes if self.cfg.flow else 0))
         paired = self.ring == "seamless" and self.with_potential
         if paired and plane_bytes >= self.RELOCATE_MIN_BYTES and (tuning is not None or autotune):
             self._relocate_partner(self.PARTNER_TRIES if plane_bytes >= self.REPLACE_MIN_BYTES
@@ -177,7 +175,7 @@ class FFMPVec:
         plane = N * G2 * self._fes
         if N * G2 * 12 < self.AUTOTUNE_MIN_BYTES:  # (the f32 layout's bytes: same choice for both formats)
             return 2
-        other = N * G2 * ((self._pes if self.with_potential else 0) + (8 if cfg.flow else 0))
+        other = N * G2 * ((self._pes if self.with_potential else 0) + (2 * self._pes if cfg.flow else 0))
         free, _ = torch.cuda.mem_get_info(self.device)
         budget = self.WINDOW_HBM_FRACTION * free - other
         return int(max(2, min(self.WINDOW_DEFAULT, budget // plane)))
@@ -192,7 +190,7 @@ class FFMPVec:
             ("frames", (N, 2, G, G) if self.frame_window == 2 else (self.frame_window, N, G, G),
              self._frame_dtype),
             ("potential", (N, G, G), self._pot_dtype),
-            ("flow", (N, 2, G, G), f32),
+            ("flow", (N, 2, G, G), self._pot_dtype),  # float16 in the compact layout, like the potential
             # state
             ("pose", (N, 3), f64), ("goal", (N, 2), f64), ("d0", (N,), f64),
             ("obst", (N, max(K, 1), 4), f64), ("obst_r", (N, max(K, 1)), f64),
@@ -536,7 +534,7 @@ class FFMPVec:
         slot/plane pairing makes one step in W ~25 % slower, profiles/r01_ring.txt §6), so a
         placement check must see all of them."""
         plane_bytes = self.state_m.numel() * (self._fes + (self._pes / 2 if self.with_potential else 0.0) +
-                                              (4.0 if self.flow is not None else 0.0))
+                                              (float(self._pes) if self.flow is not None else 0.0))
         steps = 3 if plane_bytes >= (8 << 30) else 12
         cyc = {"wrap": self.frame_window - 1, "seamless": self.frame_window}.get(self.ring, 1)
         return -(-steps // cyc) * cyc
@@ -734,7 +732,7 @@ class FFMPVec:
         reset during a newest-only launch: one frame each, added by bench.py from the episode counts)."""
         G2 = self.cfg.grid * self.cfg.grid
         per = (2 if full else 1) * self._fes * G2 + (self._pes * G2 if self.potential is not None else 0) + \
-            (8 * G2 if self.flow is not None else 0) + 4 * self.cfg.record_len()
+            (2 * self._pes * G2 if self.flow is not None else 0) + 4 * self.cfg.record_len()
         return n * per
 
     def _raster_launch(self, full: bool, mask=None, timing: Optional[list] = None) -> None:
@@ -944,7 +942,7 @@ class FFMPVec:
         if L:
             sp["lidar"] = box(-inf, inf, (L,))
         if self.flow is not None:
-            sp["flow"] = box(-inf, inf, (2, G, G))
+            sp["flow"] = box(-inf, inf, (2, G, G), np.float16 if compact else np.float32)
         return DictSpace(sp)
 
     @property

@@ -127,7 +127,8 @@ typedef struct ffmp_state {
  * consumers that convert on load — state_m frames as uint8 0/255 (the same values) and the
  * potential plane as IEEE binary16 (float32 value rounded to nearest even); the state_m and
  * potential pointers then address uint8_t / binary16 elements and the state_m strides count
- * elements.  3 instead of 8 bytes per cell of a newest-only raster.  No flow planes. */
+ * elements.  3 instead of 8 bytes per cell of a newest-only raster.  Flow planes (cfg.flow), when
+ * present, are binary16 too (obs.flow then addresses binary16 elements). */
 #define FFMP_OBS_F32 0
 #define FFMP_OBS_U8F16 1
 

@@ -135,11 +135,51 @@ def test_compact_spaces_and_learner_input():
     assert torch.allclose(q32, q8, rtol=1e-4, atol=1e-5)
 
 
-def test_compact_refuses_flow():
-    with pytest.raises(ValueError):
-        FFMPVec(4, FFMPConfig(grid=64, n_obst=4, n_beams=0, flow=True), device=DEV, obs_format="u8f16")
+def test_compact_refuses_unknown_format():
     with pytest.raises(ValueError):
         FFMPVec(4, FFMPConfig(grid=64, n_obst=4, n_beams=0), device=DEV, obs_format="f16")
+
+
+@pytest.mark.parametrize("grid", [256, 100, 512])
+def test_compact_flow_planes(grid):
+    """Flow planes in the compact layout are binary16: every compact launch shape (4 or 16 cells
+    per lane, chunks or tiles, fused or two-launch, full and newest-only launches) writes the
+    float32 run's flow planes rounded to nearest even, bit for bit, beside its frames and
+    potential; and the oracle's flow planes converted the same way."""
+    from flow_field_based_motion_planner_amd import _abi
+    from oracle.ffmp_oracle import Cfg, Record, flow_planes
+    cfg = FFMPConfig(grid=grid, n_obst=24, n_beams=16, moving=True, obst_rmax=0.7, obst_vmax=1.5, flow=True,
+                     world_half=grid * 0.05 * 0.75, max_steps=4, seed=grid + 1)
+    n = 9
+    ref = FFMPVec(n, cfg, device=DEV, autotune=False, frame_window=4)
+    ref.reset()
+    gen = torch.Generator(device=DEV).manual_seed(6)
+    acts = [torch.randint(0, 28, (n,), device=DEV, generator=gen) for _ in range(6)]
+    want = []
+    for a in acts:
+        o, _, _, _ = ref.step(a)
+        want.append((o["state_m"].to(torch.uint8), o["potential"].half(), o["flow"].half()))
+    shapes = [(sh, False) for sh in FFMPVec.COMPACT_SHAPES + ((1024, 0), (2048, _abi.RASTER_NARROW))]
+    shapes += [((0, f), True) for f in FFMPVec.COMPACT_FUSED_FLAGS]
+    for shape, fused in shapes:
+        env = FFMPVec(n, cfg, device=DEV, autotune=False, frame_window=4, obs_format="u8f16", fused=fused)
+        assert env.flow.dtype == torch.float16
+        if fused:
+            env.fused_flags = shape[1]
+        else:
+            env.raster_shape = env.raster_shape_newest = shape
+        env.reset()
+        for k, a in enumerate(acts):
+            o, _, _, _ = env.step(a)
+            assert torch.equal(o["state_m"], want[k][0]), (shape, fused, k)
+            assert _same_half(o["potential"], want[k][1]), (shape, fused, k)
+            assert _same_half(o["flow"], want[k][2]), (shape, fused, k)
+    # the oracle's flow planes of the last record, converted
+    rec = Record.unpack(env.record.cpu().numpy(), cfg.n_obst)
+    c = Cfg.from_config(cfg)
+    idx = np.arange(grid, dtype=np.float32) * c.f["res_f"] - c.f["half_f"]
+    fl = flow_planes(c, rec, idx.reshape(1, grid, 1), idx.reshape(1, 1, grid)).astype(np.float16)
+    assert np.array_equal(env.flow.cpu().numpy().view(np.uint16), fl.view(np.uint16))
 
 
 def test_raster_split_over_launches():

@@ -78,7 +78,7 @@ def test_argument_validation_no_gpu(lib):
     out2 = _abi.OutT(p, p, p, p, p)
     assert lib.ffmp_step_state(C.byref(cfg), 0, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), None) == 0
     assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == 0
-    # observation formats (FFMP_OBS_*): unknown ones, and the compact one with flow planes, are refused
+    # observation formats (FFMP_OBS_*): unknown ones are refused; the compact one takes binary16 flow planes
     ob2.format = 7
     assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == -1
     assert b"obs.format" in lib.ffmp_last_error()
@@ -87,8 +87,7 @@ def test_argument_validation_no_gpu(lib):
     assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == 0
     flow_cfg = _abi.make_cfg(FFMPConfig(grid=64, n_obst=4, n_beams=0, flow=True))
     ob2.flow = p
-    assert lib.ffmp_raster(C.byref(flow_cfg), 0, p, None, C.byref(ob2), None) == -1
-    assert b"no flow" in lib.ffmp_last_error()
+    assert lib.ffmp_raster(C.byref(flow_cfg), 0, p, None, C.byref(ob2), None) == 0
 
 
 def test_config_validation():

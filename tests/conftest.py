@@ -11,6 +11,11 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# MIOpen's first use of each convolution shape runs an exhaustive kernel search (~1-2 min per new
+# fwd+bwd shape on a fresh box, profiles/r01_network.txt); the learner tests only need correct
+# convolutions, so the suite asks for the fast search (set before torch initialises MIOpen).
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libffmp on cuda:0)")

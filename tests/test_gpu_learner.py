@@ -120,13 +120,13 @@ def test_replay_with_other_input_channels(channels):
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=64, moving=True, max_steps=6, seed=32, flow=channels == 3)
     env = FFMPVec(32, cfg, device=DEV, keep_terminal=True)
     env.reset()
-    brain = Brain(env, capacity=256, batch_size=40, seed=5, input_channels=channels)
+    brain = Brain(env, capacity=256, batch_size=48, seed=5, input_channels=channels)
     assert brain.main_q_network.conv1.in_channels == channels
     _fill(brain, env, 3)
-    idx = torch.randperm(len(brain.memory), device=DEV)[:40]
+    idx = torch.randperm(len(brain.memory), device=DEV)[:48]
     main0 = copy.deepcopy(brain.main_q_network)
     targ0 = copy.deepcopy(brain.target_q_network)
-    b, ex = brain.memory.sample(40, index=idx)
+    b, ex = brain.memory.sample(48, index=idx)
     s_in = map_channels(b.state_m, ex.get("flow"), channels).clone()
     o_in = map_channels(b.observe_m, ex.get("observe_flow"), channels).clone()
     b = type(b)(*[t.clone() for t in b])

@@ -14,6 +14,9 @@ are re-rastered there, and the Q-networks run on the batch without host round tr
       mask_terminal=True multiplies by 1 - done), MSE, Adam step
   Brain.update_target_q_network (:430-431)      -> same
 
+input_channels (train.py:66-69): 2 (default, the configuration train.py runs) = [older, newest];
+1 = the newest frame; 3 = the newest frame + the env's flow planes (network.map_channels).
+
 amp=True (not the reference's arithmetic, opt-in): the Q-network forwards (acting, replay and
 target) run under torch.autocast bfloat16 — the convolutions on the MFMA units in bf16, fp32
 accumulation, fp32 master weights, Adam state and loss (tests/test_gpu_learner.py bounds the

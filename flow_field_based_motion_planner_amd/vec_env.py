@@ -154,6 +154,7 @@ class FFMPVec:
                 self._retry_placement()
             if paired and plane_bytes >= self.RELOCATE_MIN_BYTES:
                 self._repair_slots()
+                self._recheck_fused()
             if self.placement is not None and self.ring_meta is not None:
                 self.placement = dict(self.placement, ring=self.ring_meta)
         self._needs_reset = True
@@ -642,6 +643,33 @@ class FFMPVec:
         self.fused = bool(self._fused_req) or best_ms < 0.995 * sep
         return {"chosen": self.fused, "two_launch_step_ms": round(sep, 4), "fused_step_ms": round(best_ms, 4),
                 "flags": best_f, "candidates": [[f, round(m, 4)] for m, f in res]}
+
+    def _recheck_fused(self) -> None:
+        """The one- or two-launch decision again, on the repaired ring.  _autotune_raster makes it
+        before the slot repair, whose rebuilt slots change the step time by 5-10 %, and the two
+        kinds are within ~2 % of each other at C3: on three fresh runs of one box the pre-repair
+        choice kept the two-launch step at 2.48-2.50 ms where the one-launch step ran 2.44 ms
+        (profiles/r02_fused_recheck.txt).  Two alternating rounds of two ring cycles each, the
+        better of each kind; the autotune's best fused flags; the two-launch step only if it is
+        0.5 % faster."""
+        tf = (self.placement or {}).get("fused")
+        if self._fused_req is not None or self.pipeline_slices > 1 or not tf:
+            return
+        self.reset()
+        steps = 2 * self._tune_steps()
+        ms = {False: [], True: []}
+        for _ in range(2):
+            for kind in (False, True):
+                self.fused = kind
+                self.fused_flags = tf["flags"]
+                ms[kind].append(self._raster_gbs_steady(steps)["step_ms"])
+        sep, fus = min(ms[False]), min(ms[True])
+        # ties go to the one-launch step: on the repaired ring it was the faster one on every box
+        # measured (0.3-1.4 %), the two-launch step only ahead on poorly paired rings
+        self.fused = not (sep < 0.995 * fus)
+        self._clear_after_tuning()
+        self.placement = dict(self.placement, fused=dict(tf, chosen=self.fused, recheck={
+            "two_launch_step_ms": round(sep, 4), "fused_step_ms": round(fus, 4)}))
 
     def _placement_gbs(self) -> float:
         """Cycle bandwidth of the current buffers with the current launch shapes."""

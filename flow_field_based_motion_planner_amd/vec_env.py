@@ -312,6 +312,8 @@ class FFMPVec:
         (16384, _abi.RASTER_NT | _abi.RASTER_TILE4), (8192, _abi.RASTER_NT | _abi.RASTER_TILE4),
         (8192, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4), (16384, _abi.RASTER_NT | _abi.RASTER_TILE2),
         (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (4096, _abi.RASTER_PLAIN | _abi.RASTER_TILE4),
+        # smaller tiled blocks for small planes (C2's 0.09 ms launches lose ~10 % to their last blocks)
+        (4096, _abi.RASTER_NT | _abi.RASTER_TILE4), (2048, _abi.RASTER_NT | _abi.RASTER_TILE4),
     )
 
     def _raster_gbs_steady(self, steps: int = 3) -> Dict[bool, Tuple[float, float]]:

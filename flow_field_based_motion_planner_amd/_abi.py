@@ -322,11 +322,11 @@ class SeamlessRing:
         self.lib.ffmp_ring_destroy(C.c_void_p(cur))
 
     def info(self) -> dict:
-        out = (C.c_double * 5)()
-        self.lib.ffmp_ring_info(C.c_void_p(self.handle), out, 5)
+        out = (C.c_double * 6)()
+        self.lib.ffmp_ring_info(C.c_void_p(self.handle), out, 6)
         return {"pieces": int(out[0]), "pieces_new": int(out[1]), "pair_probes": int(out[2]),
-                "pair_gbs_min": round(out[3], 1), "pair_gbs_max": round(out[4], 1), "rebuilds": self.rebuilds,
-                "reverts": self.reverts}
+                "pair_gbs_min": round(out[3], 1), "pair_gbs_max": round(out[4], 1), "pair_scale": int(out[5]),
+                "rebuilds": self.rebuilds, "reverts": self.reverts}
 
     def __del__(self):
         try:

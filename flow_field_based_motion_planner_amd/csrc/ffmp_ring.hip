@@ -69,6 +69,7 @@ struct ffmp_ring {
   std::vector<ffmp_piece> pieces;  // slot-major, slots * pieces_per_slot
   double pair_gbs_min, pair_gbs_max;  // pairing probe of the chosen pieces (0 without partner)
   int pieces_new, pieces_tested;
+  int scale;  // partner bytes per slot byte, fixed at create (RingGeom::scale; a rebuild reuses it)
 };
 
 // dlpack.h (v0.8) DLManagedTensor, the interchange torch.utils.dlpack.from_dlpack consumes
@@ -97,8 +98,9 @@ struct DLHolder_ {  // one allocation: the managed tensor, its shape/strides, it
 // two lockstep 16-B nontemporal store streams, n16 float4s to `a` and SCALE x n16 to `b`: the
 // raster's write pattern (float32 layout: frame and potential plane at the same rate, SCALE 1;
 // compact layout: 1-byte frame cells beside 2-byte potential cells, SCALE 2)
-// (every store instruction of a wave covers 1 KiB of contiguous bytes of its stream; n16 is a
-// multiple of 4096: pieces are >= 256 MiB)
+// (every store instruction of a wave covers 1 KiB of contiguous bytes of its stream).  n16 need
+// not be a multiple of 256 (the last piece beside a compact plane whose size is not): each stream
+// is bounded by its own length, n16 float4s of `a` and SCALE x n16 of `b`.
 template <int SCALE>
 __global__ __launch_bounds__(256) void pair_probe_kernel(f32x4* __restrict__ a, f32x4* __restrict__ b, int64_t n16) {
   const int64_t blk0 = (int64_t)blockIdx.x * 4096;
@@ -108,7 +110,10 @@ __global__ __launch_bounds__(256) void pair_probe_kernel(f32x4* __restrict__ a, 
     if (i >= n16) break;
     __builtin_nontemporal_store(x, a + i);
 #pragma unroll
-    for (int s = 0; s < SCALE; ++s) __builtin_nontemporal_store(x, b + SCALE * blk0 + threadIdx.x + 256 * (SCALE * k + s));
+    for (int s = 0; s < SCALE; ++s) {
+      const int64_t j = SCALE * blk0 + threadIdx.x + 256 * (SCALE * k + s);
+      if (j < SCALE * n16) __builtin_nontemporal_store(x, b + j);
+    }
   }
 }
 
@@ -117,7 +122,31 @@ namespace {
 std::mutex g_pool_mu;
 std::vector<ffmp_piece> g_pieces;   // free pieces (mapped at home), reusable
 std::vector<ffmp_piece> g_retired;  // free, but GPU work issued before their ring died may still write them
-std::atomic<double> g_ref_gbs[64][2];  // best pairing probe seen per device and partner scale 1 / 2 (choose_pieces)
+
+// Best pairing probe seen per (device, partner plane, scale) (choose_pieces' early-accept bar).
+// Keyed by the partner: a rebuild against the same plane is judged on the same scale, while a
+// relocated plane (FFMPVec._relocate_partner) or another instance starts its own reference, so one
+// high probe against some other plane cannot raise every later ring's bar.  Under g_pool_mu.
+struct PairRef { int32_t device; int scale; const void* partner; double gbs; };
+std::vector<PairRef> g_pair_ref;
+
+double pair_ref_get(int32_t device, int scale, const void* partner) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (const PairRef& p : g_pair_ref)
+    if (p.device == device && p.scale == scale && p.partner == partner) return p.gbs;
+  return 0.0;
+}
+
+void pair_ref_put(int32_t device, int scale, const void* partner, double gbs) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (PairRef& p : g_pair_ref)
+    if (p.device == device && p.scale == scale && p.partner == partner) {
+      p.gbs = std::max(p.gbs, gbs);
+      return;
+    }
+  if (g_pair_ref.size() >= 256) g_pair_ref.erase(g_pair_ref.begin());  // bounded: oldest planes first
+  g_pair_ref.push_back({device, scale, partner, gbs});
+}
 
 hipMemAllocationProp dev_prop(int32_t device) {
   hipMemAllocationProp prop = {};
@@ -265,20 +294,33 @@ bool room_for(size_t bytes) {
 int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
                   int64_t partner_bytes) {
   const int32_t device = r->device;
-  std::vector<ffmp_piece> cand;
-  // every launch issued before a retired piece's ring died has finished once this returns
-  // (the caller's DeviceScope made `device` current)
-  if (hipDeviceSynchronize() != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipDeviceSynchronize failed");
+  std::vector<ffmp_piece> cand, retired;
+  // Retired pieces become reusable only after a device synchronize that follows their
+  // retirement: snapshot (and remove) this device's retired pieces under the lock, THEN
+  // synchronize, then pool exactly that snapshot.  A ring dropped by another thread after the
+  // snapshot (e.g. a DLPack deleter while ctypes has released the GIL) stays retired until the
+  // next call, so its in-flight writes can never land in a piece handed out here.
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (size_t k = 0; k < g_retired.size();) {
       if (g_retired[k].device == device) {
-        g_pieces.push_back(g_retired[k]);
+        retired.push_back(g_retired[k]);
         g_retired.erase(g_retired.begin() + k);
       } else {
         ++k;
       }
     }
+  }
+  // every launch issued before the snapshot's rings died has finished once this returns
+  // (the caller's DeviceScope made `device` current)
+  if (hipDeviceSynchronize() != hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const ffmp_piece& p : retired) g_retired.push_back(p);
+    return fail(FFMP_E_HIP, "ffmp_ring: hipDeviceSynchronize failed");
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const ffmp_piece& p : retired) g_pieces.push_back(p);
     for (size_t k = 0; k < g_pieces.size();) {
       if (g_pieces[k].device == device && g_pieces[k].bytes == g.piece) {
         cand.push_back(g_pieces[k]);
@@ -302,8 +344,8 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
   int todo = 0;
   for (char n : need) todo += n != 0;
   const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
-  std::atomic<double>& ref_slot = g_ref_gbs[device & 63][g.scale == 2 ? 1 : 0];
-  double ref = ref_slot.load(std::memory_order_relaxed);      // best probe seen on the device: the scale "fast" is judged against
+  // best probe seen against this partner plane: the scale "fast" is judged against
+  double ref = g.pairing ? pair_ref_get(device, g.scale, partner) : 0.0;
   bool found_fast = false;
   int fresh = 0;
   hipError_t e = hipSuccess;
@@ -350,13 +392,14 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
       if (gbs >= kPairFastGBs) found_fast = true;
       if (gbs > ref) {
         ref = gbs;
-        ref_slot.store(gbs, std::memory_order_relaxed);
+        pair_ref_put(device, g.scale, partner, gbs);
       }
       if (gbs > pick_gbs) {
         pick = c;
         pick_gbs = gbs;
       }
-      // accept within 7 % of the best probe seen (this ring or an earlier one on the device), and
+      // accept within 7 % of the best probe seen against this partner plane (this ring or an earlier
+      // one / a rebuild), and
       // never below kPairFastGBs: slot 0's positions come first, and judged only against the
       // handful of probes seen so far they took badly paired pieces (round 2: slot 0 ~10 % slower
       // than every other slot on three boxes, and again after a rebuild)
@@ -412,6 +455,7 @@ int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const vo
   std::unique_ptr<ffmp_ring> r(new ffmp_ring());
   r->device = device;
   r->slots = slots;
+  r->scale = g.scale;
   r->stride = g.stride;
   r->vbytes = g.stride * (size_t)(slots + 1);
   r->pieces.resize((size_t)slots * g.per_slot);
@@ -440,9 +484,13 @@ int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partn
   RingGeom g;
   if (const int rc = ring_geom(old->device, (int64_t)old->stride, partner, partner_bytes, &g)) return rc;
   if (g.stride != old->stride) return fail(FFMP_E_ARG, "ffmp_ring_rebuild: geometry changed");
+  // the partner ratio is the ring's, fixed at create: guessing it again from old->stride (slots
+  // rounded up to whole pieces) could flip it, e.g. for compact slots of 2-2.25 GiB
+  if (partner) g.scale = old->scale;
   std::unique_ptr<ffmp_ring> r(new ffmp_ring());
   r->device = old->device;
   r->slots = old->slots;
+  r->scale = old->scale;
   r->stride = old->stride;
   r->vbytes = old->vbytes;
   r->pieces.resize(old->pieces.size());
@@ -486,7 +534,9 @@ int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap) {
   out[2] = (double)ring->pieces_tested;
   out[3] = ring->pair_gbs_min;
   out[4] = ring->pair_gbs_max;
-  return 5;
+  if (cap < 6) return 5;
+  out[5] = (double)ring->scale;
+  return 6;
 }
 
 int64_t ffmp_ring_pool_bytes(int32_t device) {

@@ -46,36 +46,38 @@ def init(backend: Optional[str] = None, device: Optional[torch.device] = None) -
 
 def _all_gather(t: torch.Tensor, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
-    if t.is_cuda:
+    if t.is_cuda and dist.get_backend(group) != "gloo":  # RCCL: one all_gather_into_tensor
         out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=group)
         return out
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t.contiguous(), group=group)
-    return torch.cat(parts)
+    # gloo (CPU tests, or several ranks rehearsed on one GPU): through host memory
+    src = t.detach().cpu().contiguous()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    return torch.cat(parts).to(t.device)
+
+
+def gather_env_rows(x: torch.Tensor, total: Optional[int] = None, group=None) -> torch.Tensor:
+    """All-gather a per-env tensor (n_local, ...) of every rank into global env order
+    (total, ...) — one collective.  Shards may differ in size by one (shard_range): each is padded
+    to the largest for the collective and unpadded afterwards.  `total`: the global env count
+    (default world * n_local)."""
+    world = dist.get_world_size(group)
+    n = x.shape[0]
+    if total is None:
+        total = n * world
+    cap = -(-total // world)
+    padded = torch.zeros((cap,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    padded[:n] = x
+    allp = _all_gather(padded, group).view((world, cap) + tuple(x.shape[1:]))
+    return torch.cat([allp[r, :shard_range(total, world, r)[1]] for r in range(world)])
 
 
 def gather_rollout(reward: torch.Tensor, done: torch.Tensor, is_goal: torch.Tensor,
                    total: Optional[int] = None, group=None) -> Dict[str, torch.Tensor]:
-    """All-gather per-env rollout scalars into global env order (one collective per call).
-
-    Shards may differ in size by one (shard_range); they are padded to the
-    largest shard for the collective and unpadded afterwards.  `total` is the
-    global env count (default: world * local count).
-    """
-    world = dist.get_world_size(group)
-    n = reward.shape[0]
-    if total is None:
-        total = n * world
-    cap = -(-total // world)
-    packed = torch.zeros(cap, 2, dtype=torch.float32, device=reward.device)
-    packed[:n, 0] = reward.float()
-    packed[:n, 1] = done.to(torch.float32) + 2.0 * is_goal.to(torch.float32)
-    allp = _all_gather(packed, group).view(world, cap, 2)
-    rows = []
-    for r in range(world):
-        _, cnt = shard_range(total, world, r)
-        rows.append(allp[r, :cnt])
-    g = torch.cat(rows)
+    """All-gather per-env rollout scalars into global env order (one collective per call):
+    reward f32 and the done / is_goal flags packed into one (n, 2) float32 row per env."""
+    packed = torch.stack([reward.float(), done.to(torch.float32) + 2.0 * is_goal.to(torch.float32)], 1)
+    g = gather_env_rows(packed, total, group)
     flags = g[:, 1].to(torch.int32)
     return {"reward": g[:, 0].contiguous(), "done": (flags & 1).bool(), "is_goal": (flags & 2).bool()}

@@ -13,6 +13,8 @@ conversions keep the reference's exact semantics:
   robot_position_extractor           odometry_to_pose: (x, y, yaw) with yaw from the quaternion
     (:157-165)                       (tf euler_from_quaternion, axes 'sxyz'), stamp -> seconds
   pose_array_callback (:126-132)     pose_array_to_start_goal: poses[0], poses[1]
+  relative_goal_calculator           relative_goal: [sqrt(dx^2 + dy^2), pi_to_pi(atan2(dy, dx)
+    (:167-180)                       - yaw)] in float64, the `relative_goal_info` rewarder2 takes
   cmd_vel_publisher (:134-143)       action_to_twist: RobotAction.cmd[a] -> linear.x, angular.z
 
 and the other direction, env -> messages: lidar_to_ranges, frame_to_image, pose_to_odometry.
@@ -91,6 +93,25 @@ def pose_array_to_start_goal(msg) -> Tuple[Tuple[float, float], Tuple[float, flo
     """pose_array_callback (train.py:126-132): start = poses[0], goal = poses[1] (x, y)."""
     s, g = msg.poses[0].position, msg.poses[1].position
     return (float(s.x), float(s.y)), (float(g.x), float(g.y))
+
+
+def _wrap_pi(a: float) -> float:
+    """ROSNode.pi_to_pi (train.py:167-172): subtract 2pi while >= pi, then add 2pi while <= -pi
+    (so both +pi and -pi end at +pi); iterative on purpose — a remainder differs in the last bits."""
+    two_pi = 2 * math.pi
+    while a >= math.pi:
+        a -= two_pi
+    while a <= -math.pi:
+        a += two_pi
+    return a
+
+
+def relative_goal(x: float, y: float, yaw: float, goal_x: float, goal_y: float) -> np.ndarray:
+    """relative_goal_calculator (train.py:174-180) on a pose (e.g. from odometry_to_pose) and the
+    goal of pose_array_to_start_goal: float64 [dist, orientation], the `relative_goal_info` that
+    FFMP.rewarder / rewarder2 consume (train.py:536, :577)."""
+    dx, dy = goal_x - x, goal_y - y
+    return np.array([math.sqrt(dx * dx + dy * dy), _wrap_pi(math.atan2(dy, dx) - yaw)])
 
 
 def action_to_twist(action: int) -> Msg:

@@ -346,7 +346,9 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
  * ffmp_kernels.hip): once a ring's last reference is gone its pieces return to a process-wide
  * pool that later rings draw from.  ffmp_ring_pool_bytes: pooled bytes (device < 0: all).
  * ffmp_ring_info: out[0..4] = pieces, fresh pieces allocated, pairing probes, min and max
- * probe GB/s of the chosen pieces (0 without a partner); returns 5. */
+ * probe GB/s of the chosen pieces (0 without a partner); with cap >= 6 also out[5] = the partner
+ * byte ratio fixed at create (1: float32 frames beside a float32 plane, 2: uint8 frames beside a
+ * binary16 plane; a rebuild keeps it).  Returns the number of values written (5 or 6). */
 typedef struct ffmp_ring ffmp_ring_t;
 int ffmp_ring_create(int32_t device, int64_t slot_bytes, int32_t slots, const void* partner,
                      int64_t partner_bytes, ffmp_ring_t** ring, void** base, int64_t* slot_stride);

@@ -185,3 +185,37 @@ def test_partner_relocation_keeps_a_consistent_env():
         act = torch.randint(0, 28, (n,), generator=g).to("cuda:0")
         oa, ob = a.step(act)[0], b.step(act)[0]
         assert torch.equal(oa["state_m"], ob["state_m"]) and torch.equal(oa["potential"], ob["potential"])
+
+
+def test_pair_probe_stays_inside_a_compact_partner_and_rebuild_keeps_the_scale():
+    """Compact ring (uint8 slots beside a binary16 plane of twice the bytes) whose last piece's
+    probe length is not a multiple of 256 float4s (G = 100): the two-stream pairing probe must not
+    write past the partner (a guard band after it keeps its bytes), and a rebuild pairs with the
+    ratio fixed at create (slots of ~2.1 GiB round up to a 3 GiB stride, from which the ratio would
+    have been guessed as 1)."""
+    free, _ = torch.cuda.mem_get_info(DEV)
+    if free < (40 << 30):
+        pytest.skip("needs ~40 GiB of free HBM")
+    G = 100
+    n = 225486                      # 2.1 GiB uint8 slot; partner 4.2 GiB
+    slot = n * G * G
+    pbytes = 2 * slot
+    last = (pbytes - 4 * (1 << 30)) // 2  # slot bytes of the last 1 GiB piece with partner beside them
+    assert last >= (64 << 20) and (last // 16) % 256 != 0
+    guard = 1 << 20
+    buf = torch.zeros(pbytes + guard, dtype=torch.uint8, device=f"cuda:{DEV}")
+    buf[pbytes:].fill_(0xA5)
+    partner = buf[:pbytes]
+    ring = _abi.SeamlessRing(DEV, (n, G, G), 3, bits=8, partner=partner)
+    torch.cuda.synchronize()
+    info = ring.info()
+    assert info["pair_scale"] == 2 and info["pieces"] == 9 and info["pair_probes"] >= 3, info
+    assert bool((buf[pbytes:] == 0xA5).all()), "pairing probe wrote past the partner"
+    ring.rebuild(0b100, partner=partner)
+    torch.cuda.synchronize()
+    assert ring.info()["pair_scale"] == 2
+    assert bool((buf[pbytes:] == 0xA5).all()), "rebuild probe wrote past the partner"
+    t = ring.tensor
+    t[3, :4].fill_(7)  # the alias slot still maps slot 0
+    torch.cuda.synchronize()
+    assert int(t[0, :4].sum()) == 7 * 4 * G * G

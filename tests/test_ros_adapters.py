@@ -79,3 +79,15 @@ def test_image_round_trip_matches_temporal_stack_input():
     st = O.TemporalStack()
     stack = st.push(back, True)  # make_temporal_maps on the first frame duplicates it
     assert stack.shape == (2, 64, 64) and np.array_equal(stack[0], stack[1])
+
+
+def test_relative_goal_adapter_on_golden(golden):
+    """ros_adapters.relative_goal reproduces the reference's relative_goal_calculator outputs
+    (generated from /root/reference/src/train.py:174-180 by tests/golden/make_golden.py) bit for bit,
+    and the pi_to_pi golden angles."""
+    for c in golden["relative_goal"]:
+        (gx, gy), (x, y, yaw) = c["goal"], c["pose"]
+        out = R.relative_goal(x, y, yaw, gx, gy)
+        assert out.dtype == np.float64 and out.tolist() == c["out"], c
+    for a, want in golden["pi_to_pi"]:
+        assert R._wrap_pi(a) == want, a

@@ -13,9 +13,14 @@ in HBM before the timed region).
 
 N=1 workload: BASELINE config C3 (32,768 envs, 256x256 grid, 16 moving discs,
 180-beam lidar) — the largest single-GPU config and the one the north-star
-target (256x256, 32k envs) is quoted on.  For N>1 each rank owns its own C3
-batch (weak scaling, no data-path collective); C4/C5 (--config) split their
-total env count over the ranks (strong scaling).  Rank 0 prints ONE JSON line.
+target (256x256, 32k envs) is quoted on.  Every run has two legs:
+
+  weak    C3 per rank (32,768 envs on each of the N GPUs) — the line's `value`
+  strong  C4: 65,536 envs split over the N ranks (`strong`; --strong-config none skips)
+
+so the driver's 1/2/4/8-GPU runs yield both scaling curves.  No data-path collective
+(env shards; one max-reduce of the timings).  --config C4/C5 makes the main leg
+split its total over the ranks instead.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -42,8 +47,12 @@ def parse():
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--flow", action="store_true", help="also raster the BEV motion-flow planes (not a BASELINE config)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=16,
-                   help="host threads of the C-oracle CPU baseline (SURVEY 8d (ii); capped at the host's CPUs)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="host threads of the C-oracle CPU baseline (SURVEY 8d (ii)); 0 = every CPU this process "
+                        "may run on (affinity mask, capped by the cgroup CPU quota)")
+    p.add_argument("--strong-config", default="C4", choices=["none", "C4", "C5"],
+                   help="second leg: this preset's TOTAL env count split over the ranks (strong scaling)")
+    p.add_argument("--strong-steps", type=int, default=None, help="timed steps of the strong leg (default --steps)")
     p.add_argument("--dump-launches", action="store_true", help="print every timed raster launch (ms) to stderr")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=None, help="env/raster pipeline slices (default: automatic)")
@@ -83,30 +92,72 @@ def _time_oracle(env, n, seconds: float, seed: int):
             return n * steps, el
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup (v2 cpu.max, else v1 cfs quota) lets this process use, or None if unlimited."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cpus() -> dict:
+    """What the host offers this process: os.cpu_count() (the whole machine), the affinity mask,
+    the cgroup quota; `usable` = the mask capped by the quota (what the CPU baseline runs on)."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 1
+    quota = _cgroup_cpus()
+    usable = max(1, min(allowed, int(quota)) if quota else allowed)
+    return {"cpu_count": os.cpu_count(), "allowed_cpus": allowed, "cgroup_cpus": quota, "usable": usable}
+
+
 def cpu_baseline(cfg, seconds: float, threads: int):
     """The C restatement of the oracle (oracle/ffmp_oracle.c, bit-identical to the NumPy oracle:
-    tests/test_oracle_c.py) stepping a bounded sample of the same workload on `threads` host
-    threads (one env per thread at a time, OpenMP over envs) — SURVEY 8(d)(ii) — plus the same on
-    one thread (8(d)(i)) and the NumPy oracle on one thread (the round-1 baseline)."""
+    tests/test_oracle_c.py) stepping a bounded sample of the same workload on every CPU this
+    process may use (threads = 0: the affinity mask capped by the cgroup quota; one env per thread
+    at a time, OpenMP over envs) — SURVEY 8(d)(ii) — plus the same on 16 threads (round 2's
+    figure), on one thread (8(d)(i)) and the NumPy oracle on one thread (the round-1 baseline)."""
     from oracle.ffmp_oracle import OracleVecEnv
     from oracle.ffmp_oracle_c import COracleVecEnv, load
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    cpus = host_cpus()
+    threads = cpus["usable"] if threads <= 0 else max(1, min(threads, cpus["allowed_cpus"]))
     # single-threaded legs first: the OpenMP pool's idle threads spin for a while after a region
     k2, el2 = _time_oracle(OracleVecEnv(cfg, 4), 4, seconds / 3, 2)
     try:
         k1, el1 = _time_oracle(COracleVecEnv(cfg, 4, threads=1), 4, seconds / 3, 1)
         n = 4 * threads
         k, el = _time_oracle(COracleVecEnv(cfg, n, threads=threads), n, seconds, 0)
+        k16 = el16 = None
+        if threads != 16:
+            k16, el16 = _time_oracle(COracleVecEnv(cfg, 64, threads=16), 64, seconds / 3, 4)
     except (OSError, RuntimeError) as exc:  # C oracle not built / not loadable here: the NumPy leg only
         k3, el3 = _time_oracle(OracleVecEnv(cfg, 4), 4, seconds, 2)
         return {"value": k3 / el3, "unit": "env-steps/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
+                "host_cpus": cpus,
                 "sample": f"4 envs x {k3 // 4} steps ({el3:.1f} s), NumPy oracle, 1 thread (C oracle unavailable: {exc})"}
     from flow_field_based_motion_planner_amd.config import preset
     c1 = preset("C1")  # BASELINE configs[0]: one env, 64x64, 4 static discs, the reference's CPU case
     k3, el3 = _time_oracle(OracleVecEnv(c1, 1), 1, 2.0, 3)
     return {"value": k / el, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": _cpu_model(),
+            "host_cpus": cpus,
             "sample": f"{n} envs x {k // n} steps of the same config ({el:.1f} s), C oracle "
-                      f"(oracle/ffmp_oracle.c, {os.path.basename(load().path)}), {threads} threads",
+                      f"(oracle/ffmp_oracle.c, {os.path.basename(load().path)}), {threads} threads "
+                      f"(every usable CPU: affinity {cpus['allowed_cpus']}, cgroup quota {cpus['cgroup_cpus']})",
+            "threads16": ({"value": k / el, "cores": 16, "sample": "the main figure (16 usable CPUs)"} if k16 is None else
+                          {"value": k16 / el16, "cores": 16, "sample": f"64 envs x {k16 // 64} steps ({el16:.1f} s), "
+                                                                         "16 threads"}),
             "one_core": {"value": k1 / el1, "cores": 1, "sample": f"4 envs x {k1 // 4} steps ({el1:.1f} s), 1 thread"},
             "numpy_one_core": {"value": k2 / el2, "cores": 1,
                                "sample": f"4 envs x {k2 // 4} steps ({el2:.1f} s), NumPy oracle OracleVecEnv, "
@@ -188,51 +239,41 @@ def time_compact(FFMPVec, name, cfg, n, dev, steps, warmup, seed):
     return out
 
 
-def main():
-    args = parse()
+def _gather_floats(vals, world, dev, backend):
+    """Every rank's `vals` (list of floats) -> (world, len) list of lists; one collective."""
     import torch
     import torch.distributed as dist
-    from flow_field_based_motion_planner_amd.config import PRESETS, bytes_per_env_step, preset
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg):
+    """Build one FFMPVec shard (timed: construct_s), W warm-up + K timed steps between barriers and
+    synchronizes, max over ranks; the dominant kernel's launches timed with HIP events on the
+    launch stream.  Returns (summary dict, env)."""
+    import torch
+    import torch.distributed as dist
+    from flow_field_based_motion_planner_amd.config import bytes_per_env_step
     from flow_field_based_motion_planner_amd.vec_env import FFMPVec
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % max(ndev, 1))
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-
-    name = args.config
-    pr = PRESETS[name]
-    cfg = preset(name, seed=args.seed, flow=args.flow)
-    strong = pr["gpus"] > 1
-    n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
-    # a strong-scaling preset (C4/C5) on fewer GPUs than it is quoted on may not fit one
-    # GPU's HBM: then every rank runs the preset's per-GPU share instead (weak scaling)
-    fb, pb = (4, 4) if args.obs_format == "f32" else (1, 2)
-    per_env = cfg.grid * cfg.grid * (2 * fb + (0 if args.no_potential else pb)) + 4096
-    budget = int(0.7 * torch.cuda.get_device_properties(dev).total_memory)
-    if not args.envs and strong and n * per_env > budget:
-        n = pr["n_envs"] // pr["gpus"]
-        strong = False
-    n_total = n * world
-    env = FFMPVec(n, cfg, device=dev, env_offset=rank * n, potential=not args.no_potential, pipeline=args.pipeline,
+    fb = 4 if args.obs_format == "f32" else 1
+    torch.cuda.synchronize(dev)
+    t_c = time.perf_counter()
+    env = FFMPVec(n, cfg, device=dev, env_offset=offset, potential=not args.no_potential, pipeline=args.pipeline,
                   frame_window=args.frame_window, seamless={"auto": None, "seamless": True, "wrap": False}[args.ring],
                   fused={"auto": None, "on": True, "off": False}[args.fused],
-                  tuning=json.load(open(args.tuning)) if args.tuning else None, obs_format=args.obs_format)
-    if args.save_tuning and rank == 0:
+                  tuning=json.load(open(args.tuning)) if (args.tuning and main_leg) else None,
+                  obs_format=args.obs_format)
+    torch.cuda.synchronize(dev)
+    construct_s = time.perf_counter() - t_c
+    if args.save_tuning and rank == 0 and main_leg:
         with open(args.save_tuning, "w") as f:
             json.dump(env.tuning(), f)
-
-    K, W = args.steps, args.warmup
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    free, total = torch.cuda.mem_get_info(dev)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank + (0 if main_leg else 5000))
     actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
     env.reset()
     for w in range(W):
@@ -253,13 +294,11 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    el_local = time.perf_counter() - t0
     env.check_errors()
     resets = int(env.episode.sum()) - ep0  # auto-resets in the timed steps
+    per_rank = _gather_floats([el_local, construct_s, float(n)], world, dev, args.dist_backend)
+    el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
 
     # the dominant kernel — the raster, or with the one-launch step the fused env-step + raster
     # kernel: HIP events around every launch on the launch stream; algorithmic bytes per launch
@@ -267,63 +306,152 @@ def main():
     # env step's state bytes), plus the older frame of every env reset during a newest-only
     # launch (resets spread evenly over launches)
     r_ms = [r[0].elapsed_time(r[1]) for r in raster_ev]
-    if args.dump_launches:
+    if args.dump_launches and main_leg:
         print("raster ms per launch:", " ".join(f"{x:.3f}" for x in r_ms), file=sys.stderr, flush=True)
     n_full = sum(1 for r in raster_ev if r[4])
     G2 = cfg.grid * cfg.grid
     r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * fb * G2
-    raster_ms = sum(r_ms) / len(r_ms)
-    step_ms_ev = ev_loop[0].elapsed_time(ev_loop[1]) / K
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
-    per_launch_envs = raster_ev[0][2]
-    placement, env_fused, env_window, env_ring, env_slices = (env.placement, bool(env.fused), env.frame_window,
-                                                              env.ring, env.pipeline_slices)
-    traffic = load_traffic(name, per_launch_envs, env.frame_window, env.ring, env.fused, args.obs_format)
+    n_total = int(sum(r[2] for r in per_rank))
+    out = {
+        "workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "scaling": "strong" if strong else "weak",
+        "value": n_total * K / el, "ms_per_step": el * 1e3 / K, "steps": K, "warmup": W,
+        "per_rank_ms_per_step": [round(r[0] * 1e3 / K, 4) for r in per_rank],
+        "per_rank_construct_s": [round(r[1], 2) for r in per_rank],
+        "construct_s": round(construct_s, 2), "hbm_bytes": env.hbm_bytes(),
+        "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
+        "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS,
+                     "kernel": "step_raster_kernel" if env.fused else "raster_kernel",
+                     "kernel_ms": sum(r_ms) / len(r_ms),
+                     "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
+                     "launches_per_step": len(r_ms) // K, "full_launches": n_full, "timed_resets": resets},
+        "raster_ms_per_step": sum(r_ms) / K,
+        "step_ms_events": ev_loop[0].elapsed_time(ev_loop[1]) / K,
+        "pipeline_slices": env.pipeline_slices,
+        "raster_autotune": env.placement,
+        "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
+        "per_launch_envs": raster_ev[0][2],
+    }
+    return out, env
+
+
+def _release(env):
+    import gc
+    import torch
+    env.close()
+    del env
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def _leg_size(name, args, world, dev):
+    """(envs per rank, strong?) for preset `name`: strong-scaling presets (C4/C5) split their total
+    over the ranks; a shard that would not fit one GPU's HBM falls back to the preset's per-GPU
+    share (weak)."""
+    import torch
+    from flow_field_based_motion_planner_amd.config import PRESETS, preset
+    pr = PRESETS[name]
+    cfg = preset(name, seed=args.seed, flow=args.flow)
+    strong = pr["gpus"] > 1
+    n = args.envs or (pr["n_envs"] // world if strong else pr["n_envs"])
+    fb, pb = (4, 4) if args.obs_format == "f32" else (1, 2)
+    per_env = cfg.grid * cfg.grid * (2 * fb + (0 if args.no_potential else pb)) + 4096
+    budget = int(0.7 * torch.cuda.get_device_properties(dev).total_memory)
+    if not args.envs and strong and n * per_env > budget:
+        n = pr["n_envs"] // pr["gpus"]
+        strong = False
+    return cfg, n, strong
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    pg_world = dist.get_world_size() if world > 1 else 1  # as the collective backend sees it
+
+    name = args.config
+    cfg, n, strong = _leg_size(name, args, world, dev)
+    K, W = args.steps, args.warmup
+    leg, env = run_leg(args, name, cfg, n, rank * n, K, W, dev, world, rank, strong, True)
+    traffic = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused, args.obs_format)
+    _release(env)
+    env = None
+
+    # second leg: the strong-scaling preset split over the ranks (SURVEY §8e: C4's 65,536 envs over
+    # 1, 2, 4, 8 GPUs), so one driver command yields both curves
+    strong_leg = None
+    if args.strong_config != "none" and args.strong_config != name and not args.tuning:
+        scfg, sn, s_strong = _leg_size(args.strong_config, args, world, dev)
+        if s_strong:
+            from flow_field_based_motion_planner_amd.distributed import shard_range
+            from flow_field_based_motion_planner_amd.config import PRESETS
+            off, sn = shard_range(PRESETS[args.strong_config]["n_envs"], world, rank)
+            strong_leg, env = run_leg(args, args.strong_config, scfg, sn, off, args.strong_steps or K, W, dev,
+                                      world, rank, True, False)
+            _release(env)
+            env = None
+            strong_leg.pop("raster_autotune", None)
+            strong_leg.pop("per_launch_envs", None)
+
     compact = None
     if world == 1 and args.obs_format == "f32" and args.compact_steps > 0 and not args.tuning \
             and not args.no_potential and not args.flow:
-        env.close()
-        del env
-        import gc
-        gc.collect()
-        torch.cuda.empty_cache()
         compact = time_compact(FFMPVec, name, cfg, n, dev, args.compact_steps, 10, args.seed)
 
     if rank == 0:
+        rl = dict(leg["roofline"], traffic=traffic)
         out = {
             "metric": METRIC,
-            "value": n_total * K / el,
+            "value": leg["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
             "warmup": W,
-            "ms_per_step": el * 1e3 / K,
+            "ms_per_step": leg["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": leg["scaling"],
             "vs_baseline": None,
             "dtype": "f32" if args.obs_format == "f32" else "u8 frames / f16 potential (f32 compute)",
             "data": "synthetic",
-            "config": {"workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "grid": cfg.grid,
+            "config": {"workload": name, "n_envs_total": leg["n_envs_total"], "n_envs_per_gpu": n, "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
-                       "frame_window": env_window, "ring": env_ring, "fused": env_fused,
+                       "frame_window": leg["frame_window"], "ring": leg["ring"], "fused": leg["fused"],
                        "parallelism": f"env-shard x{world}",
-                       "comm": (args.dist_backend if world > 1 else "none")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": traffic,
-                         "kernel": "step_raster_kernel" if env_fused else "raster_kernel", "kernel_ms": raster_ms,
-                         "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
-                         "launches_per_step": len(r_ms) // K, "full_launches": n_full,
-                         "timed_resets": resets},
-            "raster_ms_per_step": sum(r_ms) / K,
-            "step_ms_events": step_ms_ev,
-            "pipeline_slices": env_slices,
-            "raster_autotune": placement,
-            "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
+                       "comm": (args.dist_backend if world > 1 else "none"), "world_size_backend": pg_world},
+            "roofline": rl,
+            "per_rank_ms_per_step": leg["per_rank_ms_per_step"],
+            "construct_s": leg["construct_s"],
+            "per_rank_construct_s": leg["per_rank_construct_s"],
+            "hbm_bytes": leg["hbm_bytes"],
+            "hbm_in_use_bytes": leg["hbm_in_use_bytes"],
+            "raster_ms_per_step": leg["raster_ms_per_step"],
+            "step_ms_events": leg["step_ms_events"],
+            "pipeline_slices": leg["pipeline_slices"],
+            "raster_autotune": leg["raster_autotune"],
+            "hbm_roofline_pct_whole_step": leg["hbm_roofline_pct_whole_step"],
         }
+        if strong_leg is not None:
+            out["strong"] = strong_leg
         if compact is not None:
             out["compact_layout"] = compact
         if world == 1 and args.cpu_seconds > 0:

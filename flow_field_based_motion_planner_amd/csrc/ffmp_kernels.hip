@@ -40,6 +40,7 @@ __attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
   va_end(ap);
   return code;
 }
+int32_t ring_extra_swap(int32_t v);  // ffmp_ring.hip (FFMP_TUNE_RING_EXTRA)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1290,6 +1291,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       prev = t.env_lanes;
       t.env_lanes = value;
       return prev;
+    case FFMP_TUNE_RING_EXTRA:
+      if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");
+      return ffmp_detail::ring_extra_swap(value);
     default:
       return fail(FFMP_E_ARG, "unknown tuning key %d", key);
   }

@@ -15,6 +15,10 @@
 
 namespace ffmp_detail {
 int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_error())
+
+// FFMP_TUNE_RING_EXTRA: fresh pieces beyond need per create / rebuild (0 = default, v = cap v - 1)
+std::atomic<int32_t> g_ring_extra{0};
+int32_t ring_extra_swap(int32_t v) { return g_ring_extra.exchange(v); }
 }
 using ffmp_detail::fail;
 
@@ -343,7 +347,9 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
   }
   int todo = 0;
   for (char n : need) todo += n != 0;
-  const int max_new = todo + todo / 2 + 4;  // fresh pieces beyond need are the price of pairing
+  // fresh pieces beyond need are the price of pairing (capped under an HBM budget)
+  const int32_t extra = ffmp_detail::g_ring_extra.load();
+  const int max_new = todo + (extra > 0 ? extra - 1 : todo / 2 + 4);
   // best probe seen against this partner plane: the scale "fast" is judged against
   double ref = g.pairing ? pair_ref_get(device, g.scale, partner) : 0.0;
   bool found_fast = false;

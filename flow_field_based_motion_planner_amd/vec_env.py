@@ -70,6 +70,13 @@ class FFMPVec:
         tuning: a previous instance's `tuning()` (launch shapes, one- or two-launch step): used
             instead of the autotune (e.g. for profiling runs that should contain only timed
             launches); the seamless ring's slot repair still runs.
+        hbm_budget: bytes of HBM this instance may hold, at steady state and while it is built
+            (autotune placement tries and the ring's pairing candidates included): caps the frame
+            window W, the ring's extra pairing pieces (FFMP_TUNE_RING_EXTRA) and the relocation /
+            placement retries (each holds another arena + a spacer).  None: W and the retries are
+            sized from free HBM (60 % for the ring).  Pieces a closed instance's ring left in the
+            process pool are reused by later rings and are not charged to this one.  `hbm_bytes()`
+            / `hbm_peak_bytes` report what it holds / held at most.
         obs_format: "f32" (default): the reference consumer layout, state_m float32 0/255
             (train.py:543-545) and a float32 potential plane.  "u8f16": the compact layout
             (include/ffmp.h FFMP_OBS_U8F16) for consumers that convert on load — state_m uint8
@@ -83,7 +90,8 @@ class FFMPVec:
                  potential: bool = True, seed: Optional[int] = None, arena: bool = True,
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
                  frame_window: Optional[int] = None, seamless: Optional[bool] = None,
-                 fused: Optional[bool] = None, tuning: Optional[dict] = None, obs_format: str = "f32"):
+                 fused: Optional[bool] = None, tuning: Optional[dict] = None, obs_format: str = "f32",
+                 hbm_budget: Optional[int] = None):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -108,6 +116,8 @@ class FFMPVec:
         self._pes = torch.empty((), dtype=self._pot_dtype).element_size()    # bytes per potential cell
         self.env_offset = int(env_offset)
         self.with_potential = bool(potential)
+        self.hbm_budget = None if hbm_budget is None else int(hbm_budget)
+        self.hbm_peak_bytes = 0
         self.arena = bool(arena)
         self.keep_terminal = bool(keep_terminal)
         self.placement = None
@@ -166,20 +176,50 @@ class FFMPVec:
     WINDOW_DEFAULT = 8
     WINDOW_HBM_FRACTION = 0.6  # auto window: frames + other planes within this share of free HBM
 
+    def _arena_estimate(self, with_frames: bool) -> int:
+        """Bytes of the arena _alloc carves (2 MiB-aligned buffers)."""
+        off = 0
+        for _, shape, dtype in self._buffer_specs(with_frames=with_frames):
+            off = -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN + self._nbytes(shape, dtype)
+        return -(-off // self._ARENA_ALIGN) * self._ARENA_ALIGN
+
+    @staticmethod
+    def _ring_piece(slot_bytes: int) -> int:
+        """Piece size of a seamless ring slot (ffmp_ring.hip ring_geom; 2 MiB granularity)."""
+        g = 2 << 20
+        slot = -(-slot_bytes // g) * g
+        return (1 << 30) if slot >= (2 << 30) else slot
+
+    def _ring_stride(self, slot_bytes: int) -> int:
+        piece = self._ring_piece(slot_bytes)
+        return -(-slot_bytes // piece) * piece
+
     def _pick_window(self, w: Optional[int]) -> int:
-        if w is not None:
-            if int(w) < 2:
-                raise ValueError("frame_window must be >= 2")
-            return int(w)
         cfg, N = self.cfg, self.num_envs
         G2 = cfg.grid * cfg.grid
         plane = N * G2 * self._fes
+        budget = self.hbm_budget
+        if budget is not None:  # what fits: the arena (other planes, state) + W ring slots
+            rest = budget - self._arena_estimate(with_frames=False)
+            w_fit = rest // self._ring_stride(plane)
+            if rest < 2 * plane:
+                raise ValueError(f"hbm_budget {budget} B cannot hold {N} envs' planes "
+                                 f"({self._arena_estimate(with_frames=False) + 2 * plane} B at W = 2)")
+        if w is not None:
+            if int(w) < 2:
+                raise ValueError("frame_window must be >= 2")
+            if budget is not None and int(w) > 2 and int(w) > w_fit:
+                raise ValueError(f"frame_window={w} does not fit hbm_budget={budget} (at most {w_fit})")
+            return int(w)
         if N * G2 * 12 < self.AUTOTUNE_MIN_BYTES:  # (the f32 layout's bytes: same choice for both formats)
             return 2
         other = N * G2 * ((self._pes if self.with_potential else 0) + (2 * self._pes if cfg.flow else 0))
         free, _ = torch.cuda.mem_get_info(self.device)
-        budget = self.WINDOW_HBM_FRACTION * free - other
-        return int(max(2, min(self.WINDOW_DEFAULT, budget // plane)))
+        free += max(0, int(self.lib.ffmp_ring_pool_bytes(self.device.index)))  # parked pieces are reused
+        room = self.WINDOW_HBM_FRACTION * free - other
+        wmax = self.WINDOW_DEFAULT if budget is None else min(self.WINDOW_DEFAULT, w_fit)
+        W = int(max(2, min(wmax, room // plane)))
+        return 2 if W < 3 else W
 
     def _buffer_specs(self, with_frames: bool = True):
         """(name, shape, dtype) of every per-shard device buffer."""
@@ -188,7 +228,7 @@ class FFMPVec:
         f32, f64, i32, b = torch.float32, torch.float64, torch.int32, torch.bool
         specs = [
             # observation planes first: the big, hot, write-streamed buffers
-            ("frames", (N, 2, G, G) if self.frame_window == 2 else (self.frame_window, N, G, G),
+            ("frames", (N, 2, G, G) if getattr(self, "frame_window", 2) == 2 else (self.frame_window, N, G, G),
              self._frame_dtype),
             ("potential", (N, G, G), self._pot_dtype),
             ("flow", (N, 2, G, G), self._pot_dtype),  # float16 in the compact layout, like the potential
@@ -223,8 +263,13 @@ class FFMPVec:
         raster writes beside them (include/ffmp.h ffmp_ring_create)."""
         N, G = self.num_envs, self.cfg.grid
         torch.cuda.synchronize(self.device)  # the pairing probes write the potential plane on their own stream
+        prev_extra = None
         try:
             partner = self.potential if self.PAIR_SLOTS else None
+            if self.hbm_budget is not None:  # pairing candidates beyond need only within the budget
+                slot = N * G * G * self._fes
+                spare = self.hbm_budget - self._arena_used - self.frame_window * self._ring_stride(slot)
+                prev_extra = _abi.set_tuning(_abi.TUNE_RING_EXTRA, 1 + max(0, spare // self._ring_piece(slot)))
             self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, bits=8 * self._fes,
                                            partner=partner)
             self.frames = self._ring.tensor
@@ -234,8 +279,21 @@ class FFMPVec:
                 raise
             self._seamless_req = False  # no VMM here: the wrapping ring from now on
             return False
+        finally:
+            if prev_extra is not None:
+                _abi.set_tuning(_abi.TUNE_RING_EXTRA, prev_extra)
         self.ring = "seamless"
+        self._note_hbm()
         return True
+
+    def _note_hbm(self, extra: int = 0) -> None:
+        """Track the most HBM this instance has held (hbm_peak_bytes); `extra` = bytes held beside
+        the current buffers (placement tries, spacers)."""
+        self.hbm_peak_bytes = max(self.hbm_peak_bytes, self.hbm_bytes() + int(extra))
+
+    def _budget_allows(self, held_extra: int, more: int) -> bool:
+        """Under hbm_budget: may the instance hold `more` bytes beside its buffers and `held_extra`?"""
+        return self.hbm_budget is None or self.hbm_bytes() + held_extra + more <= self.hbm_budget
 
     def _alloc(self, keep_ring: bool = False):
         """All per-shard buffers, zero-initialised.  With arena=True (default) they are views
@@ -275,6 +333,7 @@ class FFMPVec:
             self.potential.zero_()  # the pairing probe wrote into it
         L = self.cfg.n_beams
         self.beam_cs = torch.as_tensor(beam_table(L), dtype=torch.float64).to(dev) if L > 0 else None
+        self._note_hbm()
 
     @staticmethod
     def _nbytes(shape, dtype) -> int:
@@ -367,8 +426,12 @@ class FFMPVec:
             free, _ = torch.cuda.mem_get_info(self.device)
             if free < 1.2 * self._arena_buf.numel() + (k + 1) * self.PLACEMENT_SPACER + (1 << 30):
                 break
+            held = sum(c[1].numel() for c in keep[1:]) + sum(t.numel() for t in spacers)
+            if not self._budget_allows(held, self._arena_buf.numel() + (k + 1) * self.PLACEMENT_SPACER):
+                break
             spacers.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
             self._alloc(keep_ring=True)
+            self._note_hbm(held + spacers[-1].numel())
             self._build_structs()
             gbs = self._placement_gbs()
             tries.append(round(gbs, 1))
@@ -448,6 +511,12 @@ class FFMPVec:
             free, _ = torch.cuda.mem_get_info(self.device)
             if free < self._arena_used + (k + 1) * self.PLACEMENT_SPACER + ring_bytes + (16 << 30):
                 break
+            # under hbm_budget: the arenas held so far (the best's among them) + this try's spacer,
+            # arena and ring beside the best ring
+            held_b = sum(t.numel() for t in held)
+            if self.hbm_budget is not None and ring_bytes + max(held_b, self._arena_used) + self._arena_used + \
+                    (k + 1) * self.PLACEMENT_SPACER + ring_bytes > self.hbm_budget:
+                break
             held.append(self._arena_buf)
             held.append(torch.empty((k + 1) * self.PLACEMENT_SPACER, dtype=torch.uint8, device=self.device))
             self._ring = self.frames = None  # the best ring stays referenced by `best`
@@ -457,6 +526,8 @@ class FFMPVec:
                 break
             if self.ring != "seamless" or self._ring is None:
                 break
+            self.hbm_peak_bytes = max(self.hbm_peak_bytes, ring_bytes + sum(t.numel() for t in held) +
+                                      self._arena_used + self.frame_window * self._ring.slot_stride)
             cur = snap()
             tries.append(cur["gbs"])
             if cur["gbs"] > best["gbs"]:
@@ -1064,10 +1135,15 @@ class FFMPVec:
         self._needs_reset = False
 
     def hbm_bytes(self) -> int:
+        """HBM this instance holds now: its arena plus the seamless ring's W physical slots (the
+        alias slot maps slot 0's pages again and holds nothing)."""
+        ring = 0
+        if self.ring == "seamless" and getattr(self, "_ring", None) is not None:
+            ring = self.frame_window * self._ring.slot_stride
         if self._arena_buf is not None:
-            ring = self.frame_window * self.frames.stride(0) * self._fes if self.ring == "seamless" else 0
             return self._arena_buf.numel() + ring
-        return sum(t.numel() * t.element_size() for t in vars(self).values() if isinstance(t, torch.Tensor))
+        return ring + sum(t.numel() * t.element_size() for t in vars(self).values()
+                          if isinstance(t, torch.Tensor) and not (ring and t is self.frames))
 
     def __repr__(self):
         c = self.cfg

@@ -181,6 +181,10 @@ int64_t ffmp_layout(int32_t which);
 #define FFMP_TUNE_RASTER_XCD 3  /* 1: XCD-aware block remap                                */
 #define FFMP_TUNE_ENV_WAVES 4   /* waves per env_kernel block: 1 or 4                       */
 #define FFMP_TUNE_ENV_LANES 5   /* lanes per env in env_kernel: 0 auto, 16, 32, 64 (>= K)   */
+#define FFMP_TUNE_RING_EXTRA 6  /* ffmp_ring_create / rebuild: fresh pieces allocated beyond the
+                                   ones the ring needs (pairing candidates; they stay pooled):
+                                   0 = default (need/2 + 4), v >= 1 = at most v - 1.  An HBM
+                                   budget (FFMPVec hbm_budget) sets it around its ring creation. */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

@@ -243,6 +243,10 @@ def test_ring_api_without_gpu(lib):
     assert lib.ffmp_ring_pool_bytes(-1) == 0
     info = (C.c_double * 5)()
     assert lib.ffmp_ring_info(None, info, 5) == -1
+    # FFMP_TUNE_RING_EXTRA: 0 = default, v = at most v - 1 extra pairing pieces; negative refused
+    assert lib.ffmp_set_tuning(_abi.TUNE_RING_EXTRA, -1) == -1
+    prev = lib.ffmp_set_tuning(_abi.TUNE_RING_EXTRA, 5)
+    assert prev == 0 and lib.ffmp_set_tuning(_abi.TUNE_RING_EXTRA, prev) == 5
 
 
 def test_exact_math_domain_validation_no_gpu(lib):

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--obs-format", default="f32", choices=["f32", "u8f16"],
                     help="u8f16: uint8 state_m / float16 potential (the Brain converts on input)")
     ap.add_argument("--amp", action="store_true", help="Q-network forwards in bfloat16 autocast (Brain(amp=True))")
+    ap.add_argument("--no-mfma", action="store_true",
+                    help="with --amp: conv2-conv4 through MIOpen instead of the MFMA kernel (conv_mfma.py)")
     ap.add_argument("--channels-last", action="store_true", help="NHWC Q-networks (Brain(channels_last=True))")
     ap.add_argument("--input-channels", type=int, default=2, choices=[1, 2, 3],
                     help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy")
@@ -55,6 +57,7 @@ def main():
                      flow=args.input_channels == 3)
     env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
+                  mfma=False if args.no_mfma else None,
                   channels_last=args.channels_last, input_channels=args.input_channels)
     obs = env.reset()
     tracker = EpisodeTracker(args.envs, device=dev)
@@ -85,7 +88,7 @@ def main():
     env.check_errors()
     summ = tracker.summary()
     out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "warmup_seconds": t_warm - t0,
-           "envs": args.envs, "steps": args.steps, "amp": args.amp, "channels_last": args.channels_last,
+           "envs": args.envs, "steps": args.steps, "amp": args.amp, "mfma": bool(brain.mfma and args.amp), "channels_last": args.channels_last,
            "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],
            "replay_bytes": brain.memory.hbm_bytes(), "replay_len": len(brain.memory), **summ}
     print(json.dumps(out))

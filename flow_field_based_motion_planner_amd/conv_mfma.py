@@ -1,0 +1,174 @@
+"""The learner's dominant convolution on the MI355X matrix cores (include/ffmp.h
+ffmp_conv2d_fwd_bf16).
+
+The reference Network (/root/reference/src/train.py:231-303) is four stride-1 convolutions and
+four linears; conv2 = nn.Conv2d(32, 64, kernel_size=32) (train.py:235) is ~80 % of its FLOPs
+(6.06 GFLOP per sample forward at the reference's 100 x 100 map).  Under `Brain(amp=True)` it runs
+here as a hand-written implicit-GEMM kernel on v_mfma_f32_32x32x16_bf16 — bf16 operands, fp32
+accumulation, bias + ReLU fused — instead of MIOpen (whose first use of each shape also runs a
+minutes-long kernel search on a fresh box).  The arithmetic is autocast's: bf16 inputs and
+weights, fp32 accumulation, a bf16 result.
+
+`MFMAConv2dReLU` is the autograd function `relu(conv2d(x, w, b))`: forward through the kernel;
+backward masks the gradient with the saved output, computes the input gradient with the same
+kernel (the "full" convolution of the masked gradient: implicit zero padding k - 1, the kernel
+flipped and transposed) and the weight / bias gradients with aten.convolution_backward on the
+same bf16 operands (MIOpen).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _abi
+
+CONV_RELU, CONV_OUT_BF16 = 1, 2  # include/ffmp.h FFMP_CONV_*
+
+
+def supported(conv: torch.nn.Conv2d) -> bool:
+    """Stride 1, no padding / dilation / groups, 32 or 64 channels in and out (the kernel's shapes)."""
+    return (conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.in_channels in (32, 64) and conv.out_channels in (32, 64) and conv.padding_mode == "zeros")
+
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """torch's [N][C][KH][KW] weight -> the kernel's bf16 [KH][KW][N][C]."""
+    return w.detach().to(torch.bfloat16).permute(2, 3, 0, 1).contiguous()
+
+
+def pack_weight_dgrad(w: torch.Tensor) -> torch.Tensor:
+    """The data gradient's kernel: w'[ky][kx][c][n] = w[n][c][KH-1-ky][KW-1-kx] (bf16)."""
+    return w.detach().to(torch.bfloat16).flip(2, 3).permute(2, 3, 1, 0).contiguous()
+
+
+def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
+                out_dtype: torch.dtype = torch.float32, pad: int = 0, dx: int = 1) -> torch.Tensor:
+    """y[b, yo, xo, n] = act(bias[n] + sum x[b, yo+ky, xo+kx*dx, c] w[ky, kx, n, c]) for an NHWC
+    bf16 x [B, H, W, C] (zero-padded by `pad` cells on every side) and a packed weight
+    [KH, KW, N, C]; returns NHWC [B, H+2pad-KH+1, W+2pad-(KW-1)dx, N]."""
+    if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
+        raise TypeError("conv2d_nhwc takes bf16 x and packed weight")
+    if not x.is_cuda or not x.is_contiguous() or not w_packed.is_contiguous():
+        raise ValueError("conv2d_nhwc takes contiguous device tensors")
+    B, H, W, Cin = x.shape
+    KH, KW, N, Cw = w_packed.shape
+    if Cw != Cin:
+        raise ValueError(f"channel mismatch: x has {Cin}, weight {Cw}")
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("out_dtype must be float32 or bfloat16")
+    y = torch.empty((B, H + 2 * pad - KH + 1, W + 2 * pad - (KW - 1) * dx, N), dtype=out_dtype, device=x.device)
+    b = None
+    if bias is not None:
+        b = bias.detach().to(device=x.device, dtype=torch.float32).contiguous()
+    flags = (CONV_RELU if relu else 0) | (CONV_OUT_BF16 if out_dtype == torch.bfloat16 else 0)
+    lib = _abi.load()
+    stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _abi.check(lib.ffmp_conv2d_fwd_bf16(x.data_ptr(), w_packed.data_ptr(), None if b is None else b.data_ptr(),
+                                        y.data_ptr(), B, H, W, Cin, KH, KW, N, int(pad), int(dx), flags, stream),
+               "ffmp_conv2d_fwd_bf16")
+    return y
+
+
+class MFMAConv2dReLU(torch.autograd.Function):
+    """relu(conv2d(x, weight, bias)) in bf16 with fp32 accumulation; returns a bf16 NCHW-shaped
+    tensor (channels-last strides)."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
+        xb = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # NHWC (free if x is channels-last)
+        wb = pack_weight(weight)
+        y = conv2d_nhwc(xb, wb, bias, relu=True, out_dtype=torch.bfloat16)
+        ctx.save_for_backward(xb, weight, y)
+        ctx.has_bias = bias is not None
+        ctx.x_dtype = x.dtype
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor):
+        xb, weight, y = ctx.saved_tensors
+        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).contiguous()  # NHWC, masked by the ReLU
+        need = ctx.needs_input_grad
+        gx = gw = gb = None
+        if need[0]:  # the full convolution of g with the flipped, transposed kernel, on the matrix cores
+            KH = weight.shape[2]
+            gx = conv2d_nhwc(g, pack_weight_dgrad(weight), None, out_dtype=torch.bfloat16, pad=KH - 1)
+            gx = gx.permute(0, 3, 1, 2).to(ctx.x_dtype)
+        if need[1] or (ctx.has_bias and need[2]):
+            wt = weight.detach().to(torch.bfloat16)
+            _, gw, gb = torch.ops.aten.convolution_backward(
+                g.permute(0, 3, 1, 2), xb.permute(0, 3, 1, 2), wt, [wt.shape[0]] if ctx.has_bias else None, [1, 1],
+                [0, 0], [1, 1], False, [0, 0], 1, [False, bool(need[1]), bool(ctx.has_bias and need[2])])
+        gw = None if gw is None else gw.to(weight.dtype)
+        gb = None if (gb is None or not ctx.has_bias) else gb.to(torch.float32)
+        return gx, gw, gb
+
+
+def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """relu(conv(x)) through the MFMA kernel (bf16, as under autocast)."""
+    return MFMAConv2dReLU.apply(x, conv.weight, conv.bias)
+
+
+# ---------------------------------------------------------------- few-channel inputs (conv1)
+# conv1 = nn.Conv2d(2, 32, kernel_size=32) (train.py:234) reads 2 channels: a K step of 16 would be
+# mostly padding.  Folding F = 32 / C consecutive kernel columns into the channel axis —
+# x'[b, y, x, j*C + c] = x[b, c, y, x + j], w'[ky, kx', n, j*C + c] = w[n, c, ky, kx'*F + j] —
+# turns it into a 32-channel convolution with KW / F kernel columns read F cells apart (dx = F):
+#   y[b, yo, xo, n] = sum_{ky, kx', q} x'[b, yo+ky, xo+kx'*F, q] w'[ky, kx', n, q]
+# the same products and sum as the original, on the MFMA kernel.
+
+def fold_supported(conv: torch.nn.Conv2d) -> bool:
+    c = conv.in_channels
+    return (conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1
+            and c in (1, 2, 4) and conv.kernel_size[1] % (32 // c) == 0 and conv.out_channels in (32, 64))
+
+
+def fold_input(x: torch.Tensor, F: int) -> torch.Tensor:
+    """x (B, C, H, W) -> bf16 NHWC (B, H, W - F + 1, F * C) with channel j*C + c = x[:, c, :, x + j]."""
+    B, Cc, H, W = x.shape
+    xn = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # (B, H, W, C)
+    s = xn.stride()
+    v = xn.as_strided((B, H, W - F + 1, F, Cc), (s[0], s[1], s[2], s[2], s[3]))
+    return v.reshape(B, H, W - F + 1, F * Cc).contiguous()
+
+
+def pack_weight_fold(w: torch.Tensor, F: int) -> torch.Tensor:
+    """w (N, C, KH, KW) -> bf16 (KH, KW / F, N, F * C) with channel j*C + c = w[n, c, ky, kx'*F + j]."""
+    N, Cc, KH, KW = w.shape
+    v = w.detach().to(torch.bfloat16).view(N, Cc, KH, KW // F, F)       # [n, c, ky, kx', j]
+    return v.permute(2, 3, 0, 4, 1).reshape(KH, KW // F, N, F * Cc).contiguous()
+
+
+class MFMAFoldConv2dReLU(torch.autograd.Function):
+    """relu(conv2d(x, weight, bias)) for a 1/2/4-channel x on the MFMA kernel (kernel columns folded
+    into 32 channels); bf16 NCHW-shaped result (channels-last strides).  Backward: the weight and
+    bias gradients (MIOpen, bf16 operands); the input's only if asked for."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
+        F = 32 // x.shape[1]
+        y = conv2d_nhwc(fold_input(x, F), pack_weight_fold(weight, F), bias, relu=True, out_dtype=torch.bfloat16,
+                        dx=F)
+        ctx.save_for_backward(x, weight, y)
+        ctx.has_bias = bias is not None
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor):
+        x, weight, y = ctx.saved_tensors
+        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).permute(0, 3, 1, 2)
+        need = ctx.needs_input_grad
+        wt = weight.detach().to(torch.bfloat16)
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            g, x.to(torch.bfloat16), wt, [wt.shape[0]] if ctx.has_bias else None, [1, 1], [0, 0], [1, 1], False,
+            [0, 0], 1, [bool(need[0]), bool(need[1]), bool(ctx.has_bias and need[2])])
+        gx = None if gx is None else gx.to(x.dtype)
+        gw = None if gw is None else gw.to(weight.dtype)
+        gb = None if (gb is None or not ctx.has_bias) else gb.to(torch.float32)
+        return gx, gw, gb
+
+
+def fold_conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """relu(conv(x)) for a few-channel conv (the reference's conv1) through the MFMA kernel."""
+    return MFMAFoldConv2dReLU.apply(x, conv.weight, conv.bias)

@@ -20,7 +20,8 @@ input_channels (train.py:66-69): 2 (default, the configuration train.py runs) = 
 amp=True (not the reference's arithmetic, opt-in): the Q-network forwards (acting, replay and
 target) run under torch.autocast bfloat16 — the convolutions on the MFMA units in bf16, fp32
 accumulation, fp32 master weights, Adam state and loss (tests/test_gpu_learner.py bounds the
-difference to the fp32 update).
+difference to the fp32 update).  With amp, conv2-conv4 (and conv2's data gradient, ~80 % of the
+network's FLOPs) run on the hand-written MFMA kernel (conv_mfma.py; mfma=False: MIOpen's).
 """
 from __future__ import annotations
 
@@ -44,13 +45,14 @@ class Brain:
     def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
                  lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
                  seed: int = 0, amp: bool = False, channels_last: bool = False,
-                 input_channels: int = INPUT_CHANNELS):
+                 input_channels: int = INPUT_CHANNELS, mfma: Optional[bool] = None):
         self.env = env
         self.device = env.device
         self.num_actions = NUM_ACTIONS
         self.batch_size, self.gamma, self.mask_terminal = int(batch_size), float(gamma), bool(mask_terminal)
         self.replay_coupling = replay_coupling
         self.amp = bool(amp)
+        self.mfma = self.amp if mfma is None else bool(mfma)  # effective under amp only (network.py)
         self.channels_last = bool(channels_last)
         # map input per train.py:66-69 (network.map_channels): 2 = [older, newest] (default), 1 =
         # newest frame, 3 = newest frame + flow xy (needs the env's flow planes)
@@ -63,8 +65,8 @@ class Brain:
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
             torch.manual_seed(seed)
-            self.main_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g).to(self.device)
-            self.target_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g).to(self.device)
+            self.main_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g, mfma=self.mfma).to(self.device)
+            self.target_q_network = Network(self.input_channels, NUM_ACTIONS, grid=g, mfma=self.mfma).to(self.device)
         if self.channels_last:  # NHWC convolutions (same values; MIOpen picks other kernels)
             self.main_q_network.to(memory_format=torch.channels_last)
             self.target_q_network.to(memory_format=torch.channels_last)

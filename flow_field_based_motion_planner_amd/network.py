@@ -13,7 +13,11 @@ runs on a batch of env tensors already in HBM:
     coupling at B > 1; `coupling="per_sample"` uses each sample's own feature, which is what
     the reference computes for B = 1 (its acting path) and keeps samples independent.
 
-The convolutions and linears are plain library GEMMs (MIOpen / hipBLASLt through torch).
+The linears are library GEMMs (hipBLASLt through torch).  With `mfma=True` and under bfloat16
+autocast (Brain(amp=True)), every convolution + ReLU runs on the hand-written MFMA kernel instead
+of MIOpen (conv_mfma.py, include/ffmp.h ffmp_conv2d_fwd_bf16; conv1's 1-4 map channels with its
+kernel columns folded into channels; the data gradients too; the weight gradients stay MIOpen's):
+the same bf16-operand / fp32-accumulate arithmetic as autocast's conv2d.
 Input maps must be G x G with G - 90 > 0 (conv k=32,32,8 then conv4 k=8 three times); the
 reference's fc2 (6400 inputs) fixes G = 100, other G size fc2 accordingly.
 """
@@ -23,10 +27,14 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import conv_mfma
+
 
 class Network(nn.Module):
-    def __init__(self, input_channels: int = 2, outputs: int = 28, grid: int = 100, coupling: str = "reference"):
+    def __init__(self, input_channels: int = 2, outputs: int = 28, grid: int = 100, coupling: str = "reference",
+                 mfma: bool = False):
         super().__init__()
+        self.mfma = bool(mfma)
         if coupling not in ("reference", "per_sample"):
             raise ValueError("coupling must be 'reference' or 'per_sample'")
         side = grid - 31 - 31 - 7 - 3 * 7
@@ -47,19 +55,29 @@ class Network(nn.Module):
         self.fc4_ea = nn.Linear(512, outputs)  # A(s, a)
         self.fc4_ev = nn.Linear(512, 1)        # V(s)
 
+    def _conv_relu(self, conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+        """relu(conv(x)): on the MFMA kernel when enabled, under bf16 autocast, for its shapes."""
+        if self.mfma and x.is_cuda and torch.is_autocast_enabled("cuda") and \
+                torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            if conv_mfma.supported(conv):
+                return conv_mfma.conv_relu(conv, x)
+            if conv_mfma.fold_supported(conv):  # conv1: 1 / 2 / 4 map channels
+                return conv_mfma.fold_conv_relu(conv, x)
+        return F.relu(conv(x))
+
     def forward(self, state_m: torch.Tensor, state_g: torch.Tensor, state_v: torch.Tensor,
                 state_t: torch.Tensor) -> torch.Tensor:
-        x_m = F.relu(self.conv1(state_m))
-        x_m = F.relu(self.conv2(x_m))
-        x_m = F.relu(self.conv3(x_m))
+        x_m = self._conv_relu(self.conv1, state_m)
+        x_m = self._conv_relu(self.conv2, x_m)
+        x_m = self._conv_relu(self.conv3, x_m)
         x_gvt = F.relu(self.fc1(torch.cat((state_g, state_v, state_t), 1)))
         tile = x_gvt[:, x_m.shape[2] - 1]                      # the loop's last value (:263-267)
         if self.coupling == "reference":
             tile = tile[:1].expand(x_m.shape[0])               # x_gvt_[0][...]: batch element 0
         x = x_m + tile.view(-1, 1, 1, 1)
-        x = F.relu(self.conv4(x))
-        x = F.relu(self.conv4(x))
-        x = F.relu(self.conv4(x))
+        x = self._conv_relu(self.conv4, x)
+        x = self._conv_relu(self.conv4, x)
+        x = self._conv_relu(self.conv4, x)
         x = torch.flatten(x, start_dim=1)
         x = F.relu(self.fc2(x))
         x = F.relu(self.fc3(x))

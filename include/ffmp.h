@@ -285,6 +285,24 @@ int ffmp_scan_collision_f64(int64_t n, int32_t L, const double* ranges, double t
 int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits,
                           unsigned long long* mismatches, uint32_t* first_bits, void* stream);
 
+/* The learner's dominant convolution on the matrix cores (the reference
+ * Network's conv2, src/train.py:233-242 / 244-255 — nn.Conv2d(32, 64, kernel_size=32) — and any
+ * stride-1, unpadded convolution with 32 or 64 channels in and out):
+ *   y[b][p][n] = act(bias[n] + sum_{ky,kx,c} x[b][yp+ky][xp+kx][c] * w[ky][kx][n][c])
+ * x NHWC bf16 [batch][h][wd][c]; w bf16 [kh][kw][n][c] (torch's [n][c][kh][kw] permuted); bias
+ * fp32 [n] or NULL; `pad` zero cells on every side of x (0 <= pad < kh, kw; pad * c % 8 == 0);
+ * kernel column kx reads input column xo + kx * dx (dx >= 1: 1 = the plain convolution);
+ * y NHWC [batch][h+2pad-kh+1][wd+2pad-(kw-1)dx][n], fp32 or (FFMP_CONV_OUT_BF16) bf16; fp32
+ * accumulation on v_mfma_f32_32x32x16_bf16 (products exact, sums in fp32).  x and w 16-byte
+ * aligned.  With pad = k - 1 and the kernel flipped and transposed (w'[ky][kx][c][n] =
+ * w[k-1-ky][k-1-kx][n][c]) it is the data gradient of the unpadded convolution.
+ * Returns FFMP_OK or a negative code (ffmp_last_error()). */
+#define FFMP_CONV_RELU 1
+#define FFMP_CONV_OUT_BF16 2
+int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* y, int32_t batch, int32_t h,
+                         int32_t wd, int32_t c, int32_t kh, int32_t kw, int32_t n, int32_t pad, int32_t dx,
+                         int32_t flags, void* stream);
+
 /* Episode bookkeeping of the training loop, batched (one record per env, device memory).
  * Per env and per ffmp_episode_update, exactly as src/train.py:579-682 does per iteration:
  *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)

@@ -1,0 +1,153 @@
+"""The learner's MFMA convolution (include/ffmp.h ffmp_conv2d_fwd_bf16, conv_mfma.py) against a
+float64 convolution of the same bf16 operands (torch's native GPU path, MIOpen off), and the
+autograd function against autocast's bf16 conv2d.  Shapes: the reference Network's conv2
+(/root/reference/src/train.py:235: 32 -> 64 channels, k = 32, 69^2 -> 38^2), conv3/conv4-like
+(64 -> 64, k = 8), the transposed conv2 a data gradient runs (64 -> 32 over a 100^2 padded image),
+and ragged sizes whose position count is not a multiple of the 512-position tile.
+
+Tolerance (fp32 accumulation of up to 32,768 bf16 products, exact in fp32): |y - y64| <=
+5e-5 * (|x| * |w|)(same position) + 1e-6; a layout error is O(1) relative."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from flow_field_based_motion_planner_amd.conv_mfma import MFMAConv2dReLU, conv2d_nhwc, pack_weight
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ref64(xb, wp, bias, pad=0):
+    x = xb.double().permute(0, 3, 1, 2)
+    w = wp.double().permute(2, 3, 0, 1)
+    with torch.backends.cudnn.flags(enabled=False):
+        y = F.conv2d(x, w, None if bias is None else bias.double(), padding=pad)
+        a = F.conv2d(x.abs(), w.abs(), padding=pad)
+    return y.permute(0, 2, 3, 1), a.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("B,H,W,C,K,N,pad", [
+    (2, 69, 69, 32, 32, 64, 0),   # conv2
+    (3, 38, 38, 64, 8, 64, 0),    # conv3 / conv4
+    (1, 100, 100, 64, 32, 32, 0),
+    (2, 38, 38, 64, 32, 32, 31),  # conv2's data gradient (implicit padding k - 1)
+    (2, 40, 45, 32, 5, 32, 0), (1, 31, 31, 64, 8, 64, 0), (5, 33, 70, 32, 2, 64, 0), (3, 20, 24, 32, 5, 64, 2)])
+def test_conv_fwd_matches_float64(B, H, W, C, K, N, pad):
+    g = torch.Generator(device=DEV).manual_seed(B * 1000 + H + K)
+    xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn((N, C, K, K), device=DEV, generator=g) / (C * K * K) ** 0.5
+    bias = torch.randn(N, device=DEV, generator=g) * 0.1
+    wp = pack_weight(w)
+    y = conv2d_nhwc(xb, wp, bias, pad=pad)
+    ref, absref = _ref64(xb, wp, bias, pad)
+    assert y.shape == (B, H + 2 * pad - K + 1, W + 2 * pad - K + 1, N)
+    err = (y.double() - ref).abs()
+    bad = err > 5e-5 * absref + 1e-6
+    assert not bool(bad.any()), f"{int(bad.sum())} of {bad.numel()} outside tolerance, max err {float(err.max())}"
+    # fused ReLU + bf16 output: the same fp32 accumulator, rounded
+    yb = conv2d_nhwc(xb, wp, bias, relu=True, out_dtype=torch.bfloat16, pad=pad)
+    assert torch.equal(yb, torch.relu(y).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("B,C,H,N,K", [(4, 32, 69, 64, 32),   # conv2
+                                       (3, 64, 38, 64, 8),    # conv3
+                                       (3, 64, 31, 64, 8), (2, 64, 24, 64, 8), (3, 64, 17, 64, 8)])  # conv4 x 3
+def test_autograd_function_against_autocast_and_float64(B, C, H, N, K):
+    """relu(conv) of the reference Network's conv2 / conv3 / conv4 shapes: the forward within bf16
+    rounding of autocast's conv2d; the gradients (input: the MFMA kernel's full convolution;
+    weight / bias: MIOpen bf16 on the saved operands; all masked by the kernel's own output) against
+    float64 autograd of the same masked product."""
+    g = torch.Generator(device=DEV).manual_seed(7 + H)
+    conv = torch.nn.Conv2d(C, N, kernel_size=K).to(DEV)
+    x = torch.relu(torch.randn((B, C, H, H), device=DEV, generator=g)).to(torch.bfloat16).requires_grad_(True)
+    y = MFMAConv2dReLU.apply(x, conv.weight, conv.bias)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y2 = F.relu(conv(x))
+    assert y.shape == y2.shape and y.dtype == y2.dtype == torch.bfloat16
+    diff = (y.detach().float() - y2.float()).abs()
+    assert float(diff.max()) <= 0.02 * float(y2.float().abs().max())
+    gy = torch.randn(y.shape, device=DEV, generator=g).to(torch.bfloat16)
+    y.backward(gy)
+    gw, gb, gx = conv.weight.grad, conv.bias.grad, x.grad
+    assert gw.dtype == torch.float32 and gb.dtype == torch.float32 and gx.dtype == torch.bfloat16
+    # float64 reference: d/d(x, w, b) of sum(conv(x, w_bf16, b) * gy * [y > 0])
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = conv.weight.detach().to(torch.bfloat16).double().requires_grad_(True)
+    b64 = conv.bias.detach().double().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=False):
+        z = F.conv2d(x64, w64, b64)
+    (z * gy.double() * (y.detach() > 0)).sum().backward()
+    for got, ref in ((gw, w64.grad), (gb, b64.grad), (gx, x64.grad)):
+        err = (got.double() - ref).abs()
+        assert float(err.max()) <= 0.01 * float(ref.abs().max()) + 1e-6, (float(err.max()), float(ref.abs().max()))
+
+
+def test_network_mfma_against_miopen_under_autocast():
+    """The reference Network (B = 6, 100^2 maps) with conv2-conv4 on the MFMA kernel against the
+    same weights through MIOpen, both under bf16 autocast: Q-values within bf16 tolerance, and every
+    parameter gradient of a loss on them in the same direction (cosine >= 0.99) and of the same norm
+    (within 5 %).  (Elementwise agreement is not expected deep in the backward pass: the two paths
+    round each activation to bf16 independently, so ReLU masks differ where a value is ~0.)"""
+    from flow_field_based_motion_planner_amd.network import Network
+    g = torch.Generator(device=DEV).manual_seed(11)
+    torch.manual_seed(11)
+    a = Network(2, 28, mfma=True).to(DEV)
+    b = Network(2, 28, mfma=False).to(DEV)
+    b.load_state_dict(a.state_dict())
+    sm = (torch.rand((6, 2, 100, 100), device=DEV, generator=g) > 0.9).float() * 255
+    sg, sv, st = (torch.rand((6, k), device=DEV, generator=g) for k in (2, 2, 1))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        qa = a(sm, sg, sv, st).float()
+        qb = b(sm, sg, sv, st).float()
+    assert float((qa - qb).abs().max()) <= 0.03 * float(qb.abs().max()) + 1e-3
+    (qa ** 2).mean().backward()
+    (qb ** 2).mean().backward()
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        ga, gb = pa.grad.double().flatten(), pb.grad.double().flatten()
+        cos = float(ga @ gb / (ga.norm() * gb.norm() + 1e-30))
+        rel = float((ga.norm() - gb.norm()).abs() / (gb.norm() + 1e-30))
+        assert cos >= 0.99 and rel <= 0.05, (name, cos, rel)
+
+
+@pytest.mark.parametrize("B,H,W,KH,KW,dx,N", [(2, 40, 85, 32, 2, 16, 32), (3, 30, 70, 7, 3, 8, 64)])
+def test_conv_dilated_matches_float64(B, H, W, KH, KW, dx, N):
+    """Kernel columns dx cells apart (the folded form of a few-channel convolution)."""
+    g = torch.Generator(device=DEV).manual_seed(H + W)
+    xb = torch.randn((B, H, W, 32), device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn((N, 32, KH, KW), device=DEV, generator=g) / (32 * KH * KW) ** 0.5
+    y = conv2d_nhwc(xb, pack_weight(w), None, dx=dx)
+    x64 = xb.double().permute(0, 3, 1, 2)
+    w64 = w.to(torch.bfloat16).double()
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = F.conv2d(x64, w64, dilation=(1, dx)).permute(0, 2, 3, 1)
+        absref = F.conv2d(x64.abs(), w64.abs(), dilation=(1, dx)).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert not bool(((y.double() - ref).abs() > 5e-5 * absref + 1e-6).any())
+
+
+@pytest.mark.parametrize("C", [2, 1])
+def test_folded_conv1_against_float64(C):
+    """The reference Network's conv1 (C map channels -> 32, k = 32, 100^2 -> 69^2; train.py:234)
+    with its kernel columns folded into 32 channels: forward vs float64 of the same bf16 operands
+    (then ReLU, bf16), weight / bias gradients vs float64 autograd of the masked product."""
+    from flow_field_based_motion_planner_amd.conv_mfma import MFMAFoldConv2dReLU
+    g = torch.Generator(device=DEV).manual_seed(5 + C)
+    conv = torch.nn.Conv2d(C, 32, kernel_size=32).to(DEV)
+    x = (torch.rand((3, C, 100, 100), device=DEV, generator=g) > 0.85).float() * 255
+    y = MFMAFoldConv2dReLU.apply(x, conv.weight, conv.bias)
+    x64 = x.double()
+    w64 = conv.weight.detach().to(torch.bfloat16).double().requires_grad_(True)
+    b64 = conv.bias.detach().double().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=False):
+        z = F.conv2d(x64, w64, b64)
+        absz = F.conv2d(x64, w64.detach().abs()) + b64.detach().abs().view(1, -1, 1, 1)
+    want = torch.relu(z.detach())
+    assert y.shape == want.shape and y.dtype == torch.bfloat16
+    tol = 5e-5 * absz + 1e-6 + want.abs() * 2 ** -8  # + the bf16 rounding of the output
+    assert not bool(((y.double() - want).abs() > tol).any())
+    gy = torch.randn(y.shape, device=DEV, generator=g).to(torch.bfloat16)
+    y.backward(gy)
+    (z * gy.double() * (y.detach() > 0)).sum().backward()
+    for got, ref in ((conv.weight.grad, w64.grad), (conv.bias.grad, b64.grad)):
+        err = (got.double() - ref).abs()
+        assert float(err.max()) <= 0.01 * float(ref.abs().max()) + 1e-6

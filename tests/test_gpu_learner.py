@@ -88,13 +88,16 @@ def test_decide_action_epsilon_greedy():
     assert 0.3 < frac < 0.65 and first.dtype == torch.int64 and int(first.max()) < 28
 
 
-def test_amp_update_close_to_fp32():
-    """Brain(amp=True): the same update with the Q-network forwards in bfloat16 autocast — loss
-    within bf16 rounding of the fp32 update's on the same minibatch and weights, every parameter
-    moved by Adam (fp32 master weights), valid greedy actions."""
+@pytest.mark.parametrize("mfma", [True, False])
+def test_amp_update_close_to_fp32(mfma):
+    """Brain(amp=True): the same update with the Q-network forwards in bfloat16 autocast — conv2-4
+    on the MFMA kernel (mfma=True, the default with amp) or MIOpen — loss within bf16 rounding of
+    the fp32 update's on the same minibatch and weights, every parameter moved by Adam (fp32
+    master weights), valid greedy actions."""
     env = _env()
     b32 = Brain(env, capacity=256, batch_size=48, seed=3)
-    b16 = Brain(env, capacity=256, batch_size=48, seed=3, amp=True)
+    b16 = Brain(env, capacity=256, batch_size=48, seed=3, amp=True, mfma=mfma)
+    assert b16.main_q_network.mfma == mfma
     b16.memory = b32.memory
     _fill(b32, env, 3)
     idx = torch.randperm(len(b32.memory), device=DEV)[:48]

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "ffmp.h"
 
 namespace ffmp_detail {
@@ -58,29 +60,29 @@ __device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4
 }
 
 // Implicit zero padding of `pad` cells on every side: logical input rows/columns [pad, pad + H/W)
-// hold the tensor, the rest are zero.  A ring slot is Wp = W + 2 pad cells wide; its pad columns
-// are zeroed once, a row load writes the W real cells (or zeros for a row outside the tensor).
+// hold the tensor, the rest are zero.  A ring slot holds the W real cells of a row (zeros for a row
+// outside the tensor); with PAD, a lane whose logical column falls outside [pad, pad + W) reads a
+// clamped address and zeroes the fragment (a select instead of 2 pad columns of LDS per slot:
+// the data gradient's slots shrink from 100 to 38 cells, so 512-position tiles fit twice per CU).
 // The ky loop runs only over kernel rows for which some row of the tile touches the tensor, and a
 // wave skips the MFMAs of kernel rows its own positions never see (the data gradient's k - 1 zero
 // border: ~12 % of its work).  Kernel column kx reads input column xp + kx * dx (dx > 1: the
 // x-dilated form a 1- or 2-channel convolution takes after its kernel columns are folded into
 // channels, conv_mfma.fold_input).
-template <int C, int NB, int MBW>
+template <int C, int NB, int MBW, bool PAD>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int N = NB * 32;
   constexpr int PT = kWaves * MBW * 32;
-  const int Wp = W + 2 * pad;
-  const int Ho = H + 2 * pad - KH + 1, Wo = Wp - (KW - 1) * dx;
+  const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const int b = blockIdx.y;
   const int P = Ho * Wo;
   const int p0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int rowbytes = W * C * 2;      // one tensor row
-  const int slotbytes = Wp * C * 2;    // one ring slot
+  const int rowbytes = W * C * 2;      // one tensor row = one ring slot
   const int chunks = rowbytes / 16;    // <= 4 * 256 (host check)
   const int yf = p0 / Wo;
   const int yl = min(P - 1, p0 + PT - 1) / Wo;
@@ -92,22 +94,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   const int wyf = min(pw0, P - 1) / Wo, wyl = min(P - 1, pw0 + MBW * 32 - 1) / Wo;
   const int wk_lo = pw0 < P ? max(ky_lo, pad - wyl) : KH, wk_hi = min(ky_hi, pad + H - 1 - wyf);
 
-  // this lane's output positions (clamped into the image; out-of-range ones are not stored)
-  int ypos[MBW], xoff[MBW];
+  // this lane's output positions (clamped into the image; out-of-range ones are not stored):
+  // output row, and input column of kernel column 0 relative to the tensor (xp - pad)
+  int ypos[MBW], xcol[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
     const int m = min(p0 + (wave * MBW + mb) * 32 + r, P - 1);
     ypos[mb] = m / Wo;
-    xoff[mb] = (m - ypos[mb] * Wo) * C * 2 + h * 16;
-  }
-
-  if (pad > 0) {  // the pad columns of every slot, once
-    const int pchunks = pad * C * 2 / 16;
-    for (int q = threadIdx.x; q < RING * 2 * pchunks; q += 256) {
-      const int slot = q / (2 * pchunks), k = q % (2 * pchunks);
-      const int off = k < pchunks ? 16 * k : (pad + W) * C * 2 + 16 * (k - pchunks);
-      *(uint4*)(lds + slot * slotbytes + off) = uint4{0u, 0u, 0u, 0u};
-    }
+    xcol[mb] = m - ypos[mb] * Wo - pad;
   }
   auto row_src = [&](int yr) -> const char* {  // logical row -> tensor row, or nullptr (zeros)
     const int real = yr - pad;
@@ -117,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   for (int row = yf + ky_lo; row <= yl + ky_lo; ++row) {
     uint4 buf[4];
     load_row_regs<C>(row_src(row), chunks, buf);
-    store_row_lds(lds + (row % RING) * slotbytes + pad * C * 2, chunks, buf);
+    store_row_lds(lds + (row % RING) * rowbytes, chunks, buf);
   }
   __syncthreads();
 
@@ -146,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
     if (ky >= wk_lo && ky <= wk_hi) {
       int aoff[MBW];
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * slotbytes + xoff[mb];
+      for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * rowbytes + h * 16;
       for (int kx = 0; kx < KW; ++kx) {
         // the next tap: (ky, kx + 1), else (ky + 1, 0) while the wave has rows left (the last
         // tap re-reads its own)
@@ -157,12 +151,22 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
 #pragma unroll
           for (int s = 0; s < C / 16; ++s)
             bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
-        const int coff = kx * dx * C * 2;
+        int coff[MBW];
+        bool cok[MBW];
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb) {
+          const int col = xcol[mb] + kx * dx;
+          cok[mb] = !PAD || (unsigned)col < (unsigned)W;
+          coff[mb] = (PAD ? min(max(col, 0), W - 1) : col) * C * 2;
+        }
 #pragma unroll
         for (int s = 0; s < C / 16; ++s) {
           bf16x8 a[MBW];
 #pragma unroll
-          for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + aoff[mb] + coff + s * 32);
+          for (int mb = 0; mb < MBW; ++mb) {
+            a[mb] = *(const bf16x8*)(lds + aoff[mb] + coff[mb] + s * 32);
+            if (PAD && !cok[mb]) a[mb] = bf16x8{};
+          }
 #pragma unroll
           for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
           for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
       }
     }
-    if (more) store_row_lds(lds + ((yl + ky + 1) % RING) * slotbytes + pad * C * 2, chunks, nrow);
+    if (more) store_row_lds(lds + ((yl + ky + 1) % RING) * rowbytes, chunks, nrow);
     __syncthreads();
   }
 
@@ -204,49 +208,199 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   }
 }
 
-// positions per workgroup: 512 (MBW 4), 256 or 128 — the fewest padded positions per image
-// (ties to the larger tile); 256 at most when a 512-position ring would not leave room for two
-// workgroups per CU (the data gradient's 100-cell padded rows)
-int pick_mbw(int P, int Wo, size_t slotbytes) {
-  int best = 4;
-  long best_pad = -1;
-  for (int mbw : {4, 2, 1}) {
-    const int pt = kWaves * mbw * 32;
-    const size_t ring = (size_t)((pt + Wo - 1) / Wo + 2) * slotbytes;
-    if (ring > 80 * 1024 && mbw > 1) continue;
-    const long padded = (long)((P + pt - 1) / pt) * pt;
-    if (best_pad < 0 || padded < best_pad) best = mbw, best_pad = padded;
+// Small images (the reference Network's conv3 / conv4: 8 x 8 kernels over 38^2 .. 17^2 maps, and
+// their data gradients): a 512-position tile wastes most of its positions on a 10^2 or 17^2
+// image, and 128-position tiles leave each wave one 32-position block (every B fragment used
+// once).  Here a workgroup owns 128 positions x all N channels and its 4 waves split the K loop
+// instead (wave w takes kernel rows ky = w, w + 4, ...), each holding all 4 position blocks x NB
+// channel blocks; the input window of the tile (all its rows for every ky) is staged in LDS once,
+// and the 4 partial accumulators are summed through LDS in the epilogue.
+template <int C, int NB, bool PAD>
+__global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
+                                                            const float* __restrict__ bias, void* __restrict__ y,
+                                                            int H, int W, int KH, int KW, int pad, int dx, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int N = NB * 32, MBW = 4, PT = 128;
+  const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
+  const int b = blockIdx.y;
+  const int P = Ho * Wo;
+  const int p0 = blockIdx.x * PT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int rowbytes = W * C * 2;
+  const int chunks = rowbytes / 16;
+  const int yf = p0 / Wo;
+  const int yl = min(P - 1, p0 + PT - 1) / Wo;
+  const char* xb = (const char*)x + (size_t)b * H * rowbytes;
+  const int ky_lo = max(0, pad - yl), ky_hi = min(KH - 1, pad + H - 1 - yf);
+
+  // the window: logical rows [yf + ky_lo, yl + ky_hi], slot = row - yf - ky_lo
+  for (int row = yf + ky_lo; row <= yl + ky_hi; ++row) {
+    const int real = row - pad;
+    const char* src = (real >= 0 && real < H) ? xb + (size_t)real * rowbytes : nullptr;
+    for (int q = threadIdx.x; q < chunks; q += 256)
+      *(uint4*)(lds + (row - yf - ky_lo) * rowbytes + 16 * q) =
+          src ? *(const uint4*)(src + 16 * (size_t)q) : uint4{0u, 0u, 0u, 0u};
   }
-  return best;
+  int ypos[MBW], xcol[MBW];
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb) {
+    const int m = min(p0 + mb * 32 + r, P - 1);
+    ypos[mb] = m / Wo - yf - ky_lo;  // window slot of kernel row ky_lo
+    xcol[mb] = m % Wo - pad;
+  }
+  __syncthreads();
+
+  f32x16 acc[MBW][NB];
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x16{};
+
+  for (int ky = ky_lo + wave; ky <= ky_hi; ky += kWaves) {
+    int aoff[MBW];
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) aoff[mb] = (ypos[mb] + ky) * rowbytes + h * 16;
+    bf16x8 bcur[NB][C / 16];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int s = 0; s < C / 16; ++s)
+        bcur[nb][s] = *(const bf16x8*)(w + ((size_t)(ky * KW * N + nb * 32 + r) * C + s * 16 + h * 8));
+    for (int kx = 0; kx < KW; ++kx) {
+      const int tn = ky * KW + min(kx + 1, KW - 1);
+      bf16x8 bnext[NB][C / 16];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int s = 0; s < C / 16; ++s)
+          bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
+      int coff[MBW];
+      bool cok[MBW];
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) {
+        const int col = xcol[mb] + kx * dx;
+        cok[mb] = !PAD || (unsigned)col < (unsigned)W;
+        coff[mb] = (PAD ? min(max(col, 0), W - 1) : col) * C * 2;
+      }
+#pragma unroll
+      for (int s = 0; s < C / 16; ++s) {
+        bf16x8 a[MBW];
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb) {
+          a[mb] = *(const bf16x8*)(lds + aoff[mb] + coff[mb] + s * 32);
+          if (PAD && !cok[mb]) a[mb] = bf16x8{};
+        }
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bcur[nb][s], acc[mb][nb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
+    }
+  }
+
+  // sum the 4 waves' partials through LDS, one channel block at a time: red[wave][mb][i][lane]
+  const bool relu = flags & FFMP_CONV_RELU, out_bf16 = flags & FFMP_CONV_OUT_BF16;
+  float* red = (float*)lds;
+  constexpr int E = MBW * 16 * 64;  // entries per wave
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    __syncthreads();  // the window (nb = 0) or the previous block's sums are no longer read
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[wave * E + (mb * 16 + i) * 64 + lane] = acc[mb][nb][i];
+    __syncthreads();
+    for (int e = threadIdx.x; e < E; e += 256) {
+      const int ln = e & 63, i = (e >> 6) & 15, mb = e >> 10;
+      const int m = p0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * (ln >> 5);
+      if (m >= P) continue;
+      const int n = nb * 32 + (ln & 31);
+      float v = red[e] + red[E + e] + red[2 * E + e] + red[3 * E + e] + (bias ? bias[n] : 0.f);
+      if (relu) v = fmaxf(v, 0.f);
+      const size_t o = ((size_t)b * P + m) * N + n;
+      if (out_bf16)
+        ((__bf16*)y)[o] = (__bf16)v;
+      else
+        ((float*)y)[o] = v;
+    }
+  }
 }
 
-template <int C, int NB, int MBW>
+constexpr size_t kSmallRedBytes = 4 * 4 * 16 * 64 * sizeof(float);  // conv_small_kernel's reduction: 64 KiB
+
+// LDS bytes of conv_small_kernel's window for this shape (a 128-position tile's rows + KH - 1)
+size_t small_window_bytes(int Wo, int KH, int W, int C) {
+  return (size_t)((128 + Wo - 1) / Wo + 1 + KH - 1) * W * C * 2;
+}
+
+template <int C, int NB, bool PAD>
+int launch_small(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
+                 int dx, int flags, hipStream_t s) {
+  const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
+  const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
+  const dim3 grid((Ho * Wo + 127) / 128, B);
+  hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w,
+                     bias, y, H, W, KH, KW, pad, dx, flags);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
+  return FFMP_OK;
+}
+
+// positions per workgroup: 512 (MBW 4), 256 or 128 — the largest tile (the most reuse of each B
+// fragment) whose rounding of an image's positions costs at most 10 % more than the tightest, and
+// whose ring leaves room for two workgroups per CU
+int pick_mbw(int P, int Wo, size_t slotbytes) {
+  long padded[3], least = -1;
+  const int mbws[3] = {4, 2, 1};
+  for (int i = 0; i < 3; ++i) {
+    const int pt = kWaves * mbws[i] * 32;
+    padded[i] = (long)((P + pt - 1) / pt) * pt;
+    if (least < 0 || padded[i] < least) least = padded[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    const int pt = kWaves * mbws[i] * 32;
+    const size_t ring = (size_t)((pt + Wo - 1) / Wo + 2) * slotbytes;
+    if ((ring <= 80 * 1024 || mbws[i] == 1) && padded[i] * 10 <= least * 11) return mbws[i];
+  }
+  return 1;
+}
+
+template <int C, int NB, int MBW, bool PAD>
 int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW,
                    int pad, int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   constexpr int PT = kWaves * MBW * 32;
   const int span = (PT + Wo - 1) / Wo + 1;  // input rows a tile reads for one ky
   const int ring = span + 1;                // + the row loaded for the next ky
-  const size_t lds = (size_t)ring * (W + 2 * pad) * C * 2;
+  const size_t lds = (size_t)ring * W * C * 2;
   if (lds > 160 * 1024)
     return fail(FFMP_E_ARG, "ffmp_conv2d: a ring of %d input rows (%zu bytes) exceeds the 160 KiB LDS", ring, lds);
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
-  hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
+  hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
                      y, H, W, KH, KW, pad, dx, ring, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
   return FFMP_OK;
 }
 
-template <int C, int NB>
+template <int C, int NB, bool PAD>
 int launch_fwd(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
                int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
-  switch (pick_mbw(Ho * Wo, Wo, (size_t)(W + 2 * pad) * C * 2)) {
-    case 4: return launch_fwd_mbw<C, NB, 4>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-    case 2: return launch_fwd_mbw<C, NB, 2>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-    default: return launch_fwd_mbw<C, NB, 1>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+  // small images with a kernel deep enough to split over the waves: conv_small_kernel
+  if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= kSmallRedBytes && (W * C * 2) % 16 == 0)
+    return launch_small<C, NB, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+  switch (pick_mbw(Ho * Wo, Wo, (size_t)W * C * 2)) {
+    case 4: return launch_fwd_mbw<C, NB, 4, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    case 2: return launch_fwd_mbw<C, NB, 2, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    default: return launch_fwd_mbw<C, NB, 1, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
   }
 }
 
@@ -263,12 +417,17 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
     return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: bad shape (batch %d, %d x %d input, %d x %d kernel, pad %d, dx %d)",
                 batch, h, wd, kh, kw, pad, dx);
   if (((uintptr_t)x | (uintptr_t)w) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: x and w must be 16-byte aligned");
-  if ((pad * c * 2) % 16) return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: pad * c must be a multiple of 8");
   hipStream_t s = (hipStream_t)stream;
-  if (c == 32 && n == 64) return launch_fwd<32, 2>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
-  if (c == 64 && n == 64) return launch_fwd<64, 2>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
-  if (c == 64 && n == 32) return launch_fwd<64, 1>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
-  if (c == 32 && n == 32) return launch_fwd<32, 1>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
+  if (pad > 0) {  // data gradients of the 32/64-channel convolutions (c = their output channels)
+    if (c == 64 && n == 32) return launch_fwd<64, 1, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
+    if (c == 64 && n == 64) return launch_fwd<64, 2, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
+    if (c == 32 && n == 64) return launch_fwd<32, 2, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
+    if (c == 32 && n == 32) return launch_fwd<32, 1, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);
+  }
+  if (c == 32 && n == 64) return launch_fwd<32, 2, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
+  if (c == 64 && n == 64) return launch_fwd<64, 2, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
+  if (c == 64 && n == 32) return launch_fwd<64, 1, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
+  if (c == 32 && n == 32) return launch_fwd<32, 1, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
   return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: channels in/out must be 32 or 64 (got %d / %d)", c, n);
 }
 

@@ -290,7 +290,7 @@ int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits,
  * stride-1, unpadded convolution with 32 or 64 channels in and out):
  *   y[b][p][n] = act(bias[n] + sum_{ky,kx,c} x[b][yp+ky][xp+kx][c] * w[ky][kx][n][c])
  * x NHWC bf16 [batch][h][wd][c]; w bf16 [kh][kw][n][c] (torch's [n][c][kh][kw] permuted); bias
- * fp32 [n] or NULL; `pad` zero cells on every side of x (0 <= pad < kh, kw; pad * c % 8 == 0);
+ * fp32 [n] or NULL; `pad` zero cells on every side of x (0 <= pad < kh, kw);
  * kernel column kx reads input column xo + kx * dx (dx >= 1: 1 = the plain convolution);
  * y NHWC [batch][h+2pad-kh+1][wd+2pad-(kw-1)dx][n], fp32 or (FFMP_CONV_OUT_BF16) bf16; fp32
  * accumulation on v_mfma_f32_32x32x16_bf16 (products exact, sums in fp32).  x and w 16-byte

@@ -31,7 +31,11 @@ def _ref64(xb, wp, bias, pad=0):
     (3, 38, 38, 64, 8, 64, 0),    # conv3 / conv4
     (1, 100, 100, 64, 32, 32, 0),
     (2, 38, 38, 64, 32, 32, 31),  # conv2's data gradient (implicit padding k - 1)
-    (2, 40, 45, 32, 5, 32, 0), (1, 31, 31, 64, 8, 64, 0), (5, 33, 70, 32, 2, 64, 0), (3, 20, 24, 32, 5, 64, 2)])
+    (2, 40, 45, 32, 5, 32, 0), (1, 31, 31, 64, 8, 64, 0), (5, 33, 70, 32, 2, 64, 0), (3, 20, 24, 32, 5, 64, 2),
+    # the row-ring kernel with padding at each tile size (512 / 256 / 128 positions)
+    (2, 30, 30, 64, 3, 64, 2), (2, 12, 12, 64, 2, 64, 1), (2, 10, 10, 32, 2, 32, 1),
+    # the small-image kernel on data-gradient shapes: conv3's and conv4's (k - 1 = 7 zero cells)
+    (2, 31, 31, 64, 8, 64, 7), (2, 10, 10, 64, 8, 64, 7)])
 def test_conv_fwd_matches_float64(B, H, W, C, K, N, pad):
     g = torch.Generator(device=DEV).manual_seed(B * 1000 + H + K)
     xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)

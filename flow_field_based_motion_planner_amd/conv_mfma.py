@@ -12,8 +12,9 @@ weights, fp32 accumulation, a bf16 result.
 `MFMAConv2dReLU` is the autograd function `relu(conv2d(x, w, b))`: forward through the kernel;
 backward masks the gradient with the saved output, computes the input gradient with the same
 kernel (the "full" convolution of the masked gradient: implicit zero padding k - 1, the kernel
-flipped and transposed) and the weight / bias gradients with aten.convolution_backward on the
-same bf16 operands (MIOpen).
+flipped and transposed) and the weight gradient with the MFMA weight-gradient kernel
+(ffmp_conv2d_wgrad_bf16: positions along k through transposing LDS reads).  No MIOpen in the
+loop: no per-shape kernel search on a fresh box.
 """
 from __future__ import annotations
 
@@ -71,6 +72,28 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Te
     return y
 
 
+def conv2d_wgrad_nhwc(g: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dx: int = 1,
+                      chunks: Optional[int] = None) -> torch.Tensor:
+    """dW[ky, kx, n, c] = sum_{b, p} g[b, p, n] x[b, yp+ky, xp+kx*dx, c] (fp32) for NHWC bf16 g
+    [B, Ho, Wo, N] and x [B, H, W, C]: the MFMA weight-gradient kernel's per-chunk partials, summed."""
+    if g.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        raise TypeError("conv2d_wgrad_nhwc takes bf16 g and x")
+    if not (g.is_contiguous() and x.is_contiguous() and g.is_cuda and x.is_cuda):
+        raise ValueError("conv2d_wgrad_nhwc takes contiguous device tensors")
+    B, H, W, Cin = x.shape
+    Bg, Ho, Wo, N = g.shape
+    if Bg != B or Ho != H - KH + 1 or Wo != W - (KW - 1) * dx:
+        raise ValueError(f"shape mismatch: g {tuple(g.shape)}, x {tuple(x.shape)}, kernel {KH}x{KW} dx {dx}")
+    if chunks is None:  # ~512 workgroups (taps per workgroup: 16 at 32 -> 64 channels, else 8)
+        groups = KH * KW // (16 if (Cin, N) == (32, 64) else 8)
+        chunks = max(1, min(B, 512 // max(groups, 1)))
+    part = torch.empty((chunks, KH, KW, N, Cin), dtype=torch.float32, device=g.device)
+    stream = C.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    _abi.check(_abi.load().ffmp_conv2d_wgrad_bf16(g.data_ptr(), x.data_ptr(), part.data_ptr(), B, H, W, Cin, KH, KW, N,
+                                                  int(dx), int(chunks), stream), "ffmp_conv2d_wgrad_bf16")
+    return part.sum(0) if chunks > 1 else part[0]
+
+
 class MFMAConv2dReLU(torch.autograd.Function):
     """relu(conv2d(x, weight, bias)) in bf16 with fp32 accumulation; returns a bf16 NCHW-shaped
     tensor (channels-last strides)."""
@@ -95,13 +118,10 @@ class MFMAConv2dReLU(torch.autograd.Function):
             KH = weight.shape[2]
             gx = conv2d_nhwc(g, pack_weight_dgrad(weight), None, out_dtype=torch.bfloat16, pad=KH - 1)
             gx = gx.permute(0, 3, 1, 2).to(ctx.x_dtype)
-        if need[1] or (ctx.has_bias and need[2]):
-            wt = weight.detach().to(torch.bfloat16)
-            _, gw, gb = torch.ops.aten.convolution_backward(
-                g.permute(0, 3, 1, 2), xb.permute(0, 3, 1, 2), wt, [wt.shape[0]] if ctx.has_bias else None, [1, 1],
-                [0, 0], [1, 1], False, [0, 0], 1, [False, bool(need[1]), bool(ctx.has_bias and need[2])])
-        gw = None if gw is None else gw.to(weight.dtype)
-        gb = None if (gb is None or not ctx.has_bias) else gb.to(torch.float32)
+        if need[1]:  # on the matrix cores too: [KH][KW][N][C] -> torch's [N][C][KH][KW]
+            gw = conv2d_wgrad_nhwc(g, xb, weight.shape[2], weight.shape[3]).permute(2, 3, 0, 1).to(weight.dtype)
+        if ctx.has_bias and need[2]:
+            gb = g.float().sum((0, 1, 2))
         return gx, gw, gb
 
 
@@ -142,8 +162,9 @@ def pack_weight_fold(w: torch.Tensor, F: int) -> torch.Tensor:
 
 class MFMAFoldConv2dReLU(torch.autograd.Function):
     """relu(conv2d(x, weight, bias)) for a 1/2/4-channel x on the MFMA kernel (kernel columns folded
-    into 32 channels); bf16 NCHW-shaped result (channels-last strides).  Backward: the weight and
-    bias gradients (MIOpen, bf16 operands); the input's only if asked for."""
+    into 32 channels); bf16 NCHW-shaped result (channels-last strides).  Backward: the weight
+    gradient of the folded convolution on the MFMA kernel, unfolded; the input's (MIOpen) only if
+    asked for."""
 
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
@@ -157,15 +178,21 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy: torch.Tensor):
         x, weight, y = ctx.saved_tensors
-        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).permute(0, 3, 1, 2)
+        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).contiguous()  # NHWC
         need = ctx.needs_input_grad
-        wt = weight.detach().to(torch.bfloat16)
-        gx, gw, gb = torch.ops.aten.convolution_backward(
-            g, x.to(torch.bfloat16), wt, [wt.shape[0]] if ctx.has_bias else None, [1, 1], [0, 0], [1, 1], False,
-            [0, 0], 1, [bool(need[0]), bool(need[1]), bool(ctx.has_bias and need[2])])
-        gx = None if gx is None else gx.to(x.dtype)
-        gw = None if gw is None else gw.to(weight.dtype)
-        gb = None if (gb is None or not ctx.has_bias) else gb.to(torch.float32)
+        gx = gw = gb = None
+        if need[0]:  # the map input has no gradient in the Network; for completeness, MIOpen's
+            wt = weight.detach().to(torch.bfloat16)
+            gx = torch.ops.aten.convolution_backward(g.permute(0, 3, 1, 2), x.to(torch.bfloat16), wt, None, [1, 1],
+                                                     [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            gx = gx.to(x.dtype)
+        if need[1]:  # the folded kernel's weight gradient, unfolded: q = j * C + c, kx = kx' * F + j
+            N, Cc, KH, KW = weight.shape
+            F = 32 // Cc
+            gwf = conv2d_wgrad_nhwc(g, fold_input(x, F), KH, KW // F, dx=F)  # [KH][KW/F][N][F*C]
+            gw = gwf.view(KH, KW // F, N, F, Cc).permute(2, 4, 0, 1, 3).reshape(N, Cc, KH, KW).to(weight.dtype)
+        if ctx.has_bias and need[2]:
+            gb = g.float().sum((0, 1, 2))
         return gx, gw, gb
 
 

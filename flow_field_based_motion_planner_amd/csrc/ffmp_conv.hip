@@ -404,6 +404,231 @@ int launch_fwd(const void* x, const void* w, const float* bias, void* y, int B, 
   }
 }
 
+// ------------------------------------------------------------------ weight gradient
+// dW[tap][n][c] = sum_p g[p][n] * x[p + tap][c]: per tap a GEMM over positions, M = n (the output
+// gradient g, NHWC [B][Ho][Wo][N]), N = c (the saved input x, NHWC [B][H][W][C]), K = positions.
+// Both MFMA operands need positions along k, i.e. channel COLUMNS of the NHWC row images: they are
+// read with ds_read_b64_tr_b16 (per 16 lanes, 4 image rows x 16 columns delivered column-major),
+// lane (r, h) of the 32x32x16 operand getting image rows k0 + 8h .. +8 of its column r — from
+// plain NHWC rows staged in LDS, no transposition pass.  128-byte image rows XOR their 16-byte
+// chunk with ((row >> 1) & 1) << 2, so the 4 rows x 2 column halves of a 32-lane half cover all
+// 64 banks.
+//
+// A workgroup owns TG = 4 * TW taps (a TKY x TKX rectangle of kernel rows / columns) and one chunk
+// of the batch; wave w the taps [w * TW, (w + 1) * TW) of the rectangle, TW * NB * CB 32x32
+// blocks (128 accumulators).  K runs over stages of R output rows of each sample (R * Wo
+// positions, flattened, so no per-row padding): the stage's g rows and the x rows
+// [y0 + kyA, y0 + R - 1 + kyA + TKY - 1] are copied to LDS (the next stage is loaded into
+// registers while this one is consumed), then every wave walks the stage in k-steps of 16
+// positions.  Each workgroup writes its taps' partial sums for its chunk of the batch:
+// part[chunk][tap][n][c] (fp32); the caller sums over chunks.
+__device__ __forceinline__ int swz128(int row) { return ((row >> 1) & 1) << 6; }  // bytes: chunk ^ 4
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4 tr_read(const char* p) {  // ds_read_b64_tr_b16 (8-byte aligned)
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 12 * 256: host check)
+
+// Stage copies: one stage's g rows and x rows are contiguous byte ranges of g and x; piece k < gq
+// comes from g, else from x; threads past the end re-read the last piece (no divergent loads).
+// Written out in the kernel body: behind a helper taking the register array by reference,
+// hipcc (ROCm 7.2) kept the array in scratch memory.
+#define FFMP_WGRAD_LOAD1(i, gs, xs)                                                                  \
+  {                                                                                                  \
+    const int k = min((int)threadIdx.x + 256 * (i), gq + xq - 1);                                    \
+    buf##i = *(const uint4*)(k < gq ? (gs) + 16 * (size_t)k : (xs) + 16 * (size_t)(k - gq));         \
+  }
+#define FFMP_WGRAD_LOAD(gs, xs)                                                                    \
+  FFMP_WGRAD_LOAD1(0, gs, xs) FFMP_WGRAD_LOAD1(1, gs, xs) FFMP_WGRAD_LOAD1(2, gs, xs)              \
+  FFMP_WGRAD_LOAD1(3, gs, xs) FFMP_WGRAD_LOAD1(4, gs, xs) FFMP_WGRAD_LOAD1(5, gs, xs)              \
+  FFMP_WGRAD_LOAD1(6, gs, xs) FFMP_WGRAD_LOAD1(7, gs, xs) FFMP_WGRAD_LOAD1(8, gs, xs)              \
+  FFMP_WGRAD_LOAD1(9, gs, xs) FFMP_WGRAD_LOAD1(10, gs, xs) FFMP_WGRAD_LOAD1(11, gs, xs)
+// ... and into the LDS images (g rows: N * 2 bytes, x rows: C * 2 bytes; 128-byte rows swizzled)
+#define FFMP_WGRAD_STORE1(i)                                                                         \
+  {                                                                                                  \
+    const int k = (int)threadIdx.x + 256 * (i);                                                      \
+    const bool isg = k < gq;                                                                         \
+    const int kk = isg ? k : k - gq, rb = isg ? N * 2 : C * 2, row = kk / (rb / 16);                 \
+    const int off = (kk % (rb / 16)) * 16;                                                           \
+    const bool sw = isg ? N == 64 : C == 64;                                                         \
+    char* d = (isg ? gimg : ximg) + row * rb + (sw ? (off ^ swz128(row)) : off);                     \
+    if (k < gq + xq) *(uint4*)d = buf##i;                                                            \
+  }
+#define FFMP_WGRAD_STORE()                                                                         \
+  FFMP_WGRAD_STORE1(0) FFMP_WGRAD_STORE1(1) FFMP_WGRAD_STORE1(2) FFMP_WGRAD_STORE1(3)              \
+  FFMP_WGRAD_STORE1(4) FFMP_WGRAD_STORE1(5) FFMP_WGRAD_STORE1(6) FFMP_WGRAD_STORE1(7)              \
+  FFMP_WGRAD_STORE1(8) FFMP_WGRAD_STORE1(9) FFMP_WGRAD_STORE1(10) FFMP_WGRAD_STORE1(11)
+
+template <int C, int N, int TW>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
+                                                            float* __restrict__ part, int B, int H, int W, int KH,
+                                                            int KW, int dx, int TKY, int TKX, int R, int per_chunk) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int NB = N / 32, CB = C / 32;
+  const int Ho = H - KH + 1, Wo = W - (KW - 1) * dx;
+  const int groups_x = KW / TKX;
+  const int kyA = (blockIdx.x / groups_x) * TKY, kxA = (blockIdx.x % groups_x) * TKX;
+  const int b0 = blockIdx.y * per_chunk, b1 = min(B, b0 + per_chunk);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = (lane & 15) >> 2, pp = lane & 3, gh = (lane >> 4) & 1;  // tr-read: row q, columns 4pp.., half gh
+  const int grow = N * 2, xrowb = C * 2;             // image row bytes
+  const int Pmax = R * Wo;                            // positions of a full stage
+  char* gimg = lds;
+  char* ximg = lds + (Pmax + 16) * grow;              // g image + 16 zero rows (k-steps past the stage end)
+
+  // this wave's taps of the rectangle (the host makes the rectangle tile the kernel exactly);
+  // the B image row of (position row pr, column pc) at tap t: (pr + dky[t]) * W + pc + dkx[t]
+  int dky[TW], dkx[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int k = wave * TW + t;
+    dky[t] = k / TKX;
+    dkx[t] = (kxA + k % TKX) * dx;
+  }
+  for (int i = threadIdx.x; i < grow; i += 256) *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
+
+  f32x16 acc[TW][NB][CB];
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) acc[t][nb][cb] = f32x16{};
+
+  const int stages_per_sample = (Ho + R - 1) / R;
+  const int nstages = (b1 - b0) * stages_per_sample;
+  // lane-constant parts of the tr-read addresses
+  const int acol0 = (16 * gh + 4 * pp) * 2;  // + nb * 64 bytes
+  uint4 buf0, buf1, buf2, buf3, buf4, buf5, buf6, buf7, buf8, buf9, buf10, buf11;  // kWgradPieces
+  int gq = 0, xq = 0;
+  if (nstages > 0) {
+    const int y0 = 0, nr = min(R, Ho);
+    gq = nr * Wo * grow / 16;
+    xq = min(nr + TKY - 1, H - kyA) * W * xrowb / 16;
+    const char* gs = (const char*)g + ((size_t)b0 * Ho + y0) * Wo * grow;
+    const char* xs = (const char*)x + ((size_t)b0 * H + y0 + kyA) * W * xrowb;
+    FFMP_WGRAD_LOAD(gs, xs)
+  }
+  for (int st = 0; st < nstages; ++st) {
+    __syncthreads();  // the previous stage's reads are done
+    FFMP_WGRAD_STORE()
+    __syncthreads();
+    const int nr = min(R, Ho - (st % stages_per_sample) * R);
+    if (st + 1 < nstages) {  // the next stage, in flight while this one is consumed
+      const int b = b0 + (st + 1) / stages_per_sample, y0 = ((st + 1) % stages_per_sample) * R;
+      const int nr1 = min(R, Ho - y0);
+      gq = nr1 * Wo * grow / 16;
+      xq = min(nr1 + TKY - 1, H - y0 - kyA) * W * xrowb / 16;
+      const char* gs = (const char*)g + ((size_t)b * Ho + y0) * Wo * grow;
+      const char* xs = (const char*)x + ((size_t)b * H + y0 + kyA) * W * xrowb;
+      FFMP_WGRAD_LOAD(gs, xs)
+    }
+    const int Ps = nr * Wo;
+    // this lane's two k rows per k-step (u = 0, 1): position p = k0 + 8h + 4u + q, as (stage
+    // row, column), advanced by 16 per k-step without branches (Wo >= 8: host check)
+    int pr[2], pc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = 8 * h + 4 * u + q;
+      pr[u] = p / Wo;
+      pc[u] = p - pr[u] * Wo;
+    }
+    for (int k0 = 0; k0 < Ps; k0 += 16) {
+      // each operand fragment = two transposing reads (k rows 8h + 4u .. +4), joined as whole
+      // vectors (element-wise assembly of the 4 x 16-bit results miscompiles: ROCm 7.2)
+      s16x4 ar[NB][2], br[TW][CB][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = k0 + 8 * h + 4 * u + q;
+        const bool in = p < Ps;
+        const int grw = in ? p : Pmax + (p & 15);  // past the stage end: a zero row
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int col = acol0 + nb * 64;
+          const int off = N == 64 ? ((col & ~15) ^ swz128(grw)) | (col & 15) : col;
+          ar[nb][u] = tr_read(gimg + grw * grow + off);
+        }
+        const int base = in ? pr[u] * W + pc[u] : 0;
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          const int xrw = base + dky[t] * W + dkx[t];
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            const int col = acol0 + cb * 64;
+            const int off = C == 64 ? ((col & ~15) ^ swz128(xrw)) | (col & 15) : col;
+            br[t][cb][u] = tr_read(ximg + xrw * xrowb + off);
+          }
+        }
+        int c = pc[u] + 16, rr = pr[u];
+        if (c >= Wo) c -= Wo, ++rr;
+        if (c >= Wo) c -= Wo, ++rr;
+        pc[u] = c;
+        pr[u] = rr;
+      }
+      bf16x8 a[NB], bb[TW][CB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        a[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ar[nb][0], ar[nb][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          bb[t][cb] = __builtin_bit_cast(bf16x8,
+                                         __builtin_shufflevector(br[t][cb][0], br[t][cb][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb)
+            acc[t][nb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[nb], bb[t][cb], acc[t][nb][cb], 0, 0, 0);
+    }
+  }
+
+  // partial sums: part[chunk][tap][n][c]; C/D row = n ((i & 3) + 8 (i >> 2) + 4 h), column = c (r)
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int k = wave * TW + t;
+    float* dst = part + ((size_t)blockIdx.y * KH * KW + (kyA + k / TKX) * KW + kxA + k % TKX) * N * C;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int n = nb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          dst[n * C + cb * 32 + r] = acc[t][nb][cb][i];
+        }
+  }
+}
+
+template <int C, int N, int TW>
+int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W, int KH, int KW, int dx, int chunks,
+                 hipStream_t s) {
+  const int Ho = H - KH + 1, Wo = W - (KW - 1) * dx;
+  constexpr int TG = 4 * TW;
+  const int TKX = std::min(KW, TG), TKY = TG / TKX;
+  if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
+  // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
+  int R = std::min(Ho, 8);
+  auto bytes = [&](int rr) { return (size_t)(rr * Wo + 16) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
+  auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };
+  while (R > 1 && (bytes(R) > 48 * 1024 || pieces(R) > kWgradPieces * 256)) --R;
+  if (bytes(R) > 64 * 1024 || pieces(R) > kWgradPieces * 256)
+    return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: rows of %d x %d x %d do not fit one stage", W, C, N);
+  if (Wo < 8) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: output rows of %d < 8 positions", Wo);
+  const int per_chunk = (B + chunks - 1) / chunks;
+  const dim3 grid((KH / TKY) * (KW / TKX), (B + per_chunk - 1) / per_chunk);
+  hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW>), grid, dim3(256), bytes(R), s, (const __bf16*)g, (const __bf16*)x,
+                     part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d_wgrad launch: %s", hipGetErrorString(e));
+  return FFMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -429,6 +654,21 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
   if (c == 64 && n == 32) return launch_fwd<64, 1, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
   if (c == 32 && n == 32) return launch_fwd<32, 1, false>(x, w, bias, y, batch, h, wd, kh, kw, 0, dx, flags, s);
   return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: channels in/out must be 32 or 64 (got %d / %d)", c, n);
+}
+
+int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t batch, int32_t h, int32_t wd, int32_t c,
+                           int32_t kh, int32_t kw, int32_t n, int32_t dx, int32_t chunks, void* stream) {
+  if (!g || !x || !part) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: NULL tensor");
+  if (batch <= 0 || batch > 65535 || kh <= 0 || kw <= 0 || dx < 1 || h < kh || wd < (kw - 1) * dx + 1 || chunks < 1)
+    return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: bad shape (batch %d, %d x %d input, %d x %d kernel, dx %d, %d chunks)",
+                batch, h, wd, kh, kw, dx, chunks);
+  if (((uintptr_t)g | (uintptr_t)x) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: g and x must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (c == 32 && n == 64) return launch_wgrad<32, 64, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  if (c == 64 && n == 64) return launch_wgrad<64, 64, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  if (c == 32 && n == 32) return launch_wgrad<32, 32, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  if (c == 64 && n == 32) return launch_wgrad<64, 32, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: channels in/out must be 32 or 64 (got %d / %d)", c, n);
 }
 
 }  // extern "C"

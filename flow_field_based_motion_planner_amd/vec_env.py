@@ -680,11 +680,17 @@ class FFMPVec:
         (16384, _abi.RASTER_NT | _abi.RASTER_TILE16), (65536, _abi.RASTER_NT | _abi.RASTER_TILE4),
         (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (16384, _abi.RASTER_PLAIN | _abi.RASTER_TILE16),
         (32768, _abi.RASTER_PLAIN | _abi.RASTER_TILE4 | _abi.RASTER_NARROW),
+        # round 3: 4-cell lanes in 2 x 128-cell tiles or 256-cell rows, so that a wave's uint8 frame
+        # stores cover whole 128-byte lines (TILE4's 64-cell rows write half lines: PMC 1.02x)
+        (32768, _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW),
+        (65536, _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW),
+        (32768, _abi.RASTER_NT | _abi.RASTER_NARROW),
     )
     COMPACT_FUSED_FLAGS = (
         _abi.RASTER_NT | _abi.RASTER_TILE16, _abi.RASTER_NT | _abi.RASTER_TILE8, _abi.RASTER_NT | _abi.RASTER_TILE4,
         _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW, _abi.RASTER_PLAIN | _abi.RASTER_TILE16,
         _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE16, _abi.RASTER_NT,
+        _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW,
     )
 
     XCD_SHAPES = True  # autotune candidates include the XCD-aware block remap

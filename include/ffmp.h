@@ -303,6 +303,15 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
                          int32_t wd, int32_t c, int32_t kh, int32_t kw, int32_t n, int32_t pad, int32_t dx,
                          int32_t flags, void* stream);
 
+/* The weight gradient of the same convolutions (MFMA, bf16 operands, fp32 accumulation):
+ *   part[k][ky][kx][n][c] = sum over the samples of chunk k and all output positions p of
+ *                           g[b][p][n] * x[b][yp+ky][xp+kx*dx][c]
+ * g NHWC bf16 [batch][h-kh+1][wd-(kw-1)dx][n] (the output gradient), x NHWC bf16
+ * [batch][h][wd][c] (the forward input); part fp32 [chunks][kh][kw][n][c] (every element
+ * written); the caller sums over the chunks (batch split into `chunks` consecutive ranges). */
+int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t batch, int32_t h, int32_t wd, int32_t c,
+                           int32_t kh, int32_t kw, int32_t n, int32_t dx, int32_t chunks, void* stream);
+
 /* Episode bookkeeping of the training loop, batched (one record per env, device memory).
  * Per env and per ffmp_episode_update, exactly as src/train.py:579-682 does per iteration:
  *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)

@@ -155,3 +155,28 @@ def test_folded_conv1_against_float64(C):
     for got, ref in ((conv.weight.grad, w64.grad), (conv.bias.grad, b64.grad)):
         err = (got.double() - ref).abs()
         assert float(err.max()) <= 0.01 * float(ref.abs().max()) + 1e-6
+
+
+@pytest.mark.parametrize("B,H,W,C,KH,KW,N,dx", [
+    (3, 69, 69, 32, 32, 32, 64, 1),   # conv2
+    (3, 38, 38, 64, 8, 8, 64, 1),     # conv3
+    (2, 17, 17, 64, 8, 8, 64, 1),     # conv4's last
+    (2, 100, 85, 32, 32, 2, 32, 16),  # conv1 folded (2 channels, 16 kernel columns per folded column)
+    (2, 20, 20, 64, 8, 8, 32, 1), (3, 20, 22, 32, 6, 4, 32, 1)])
+def test_wgrad_matches_float64(B, H, W, C, KH, KW, N, dx):
+    """ffmp_conv2d_wgrad_bf16 (positions along k through ds_read_b64_tr_b16) against torch's float64
+    weight gradient of the same bf16 operands; tolerance as the forward's."""
+    from flow_field_based_motion_planner_amd.conv_mfma import conv2d_wgrad_nhwc
+    g0 = torch.Generator(device=DEV).manual_seed(B + H + KH + N)
+    Ho, Wo = H - KH + 1, W - (KW - 1) * dx
+    x = torch.randn((B, H, W, C), device=DEV, generator=g0).to(torch.bfloat16)
+    g = torch.randn((B, Ho, Wo, N), device=DEV, generator=g0).to(torch.bfloat16)
+    dw = conv2d_wgrad_nhwc(g, x, KH, KW, dx=dx)
+    assert dw.shape == (KH, KW, N, C) and dw.dtype == torch.float32
+    x64, g64 = x.double().permute(0, 3, 1, 2), g.double().permute(0, 3, 1, 2)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = torch.nn.grad.conv2d_weight(x64, (N, C, KH, KW), g64, dilation=(1, dx)).permute(2, 3, 0, 1)
+        absref = torch.nn.grad.conv2d_weight(x64.abs(), (N, C, KH, KW), g64.abs(), dilation=(1, dx)).permute(2, 3, 0, 1)
+    err = (dw.double() - ref).abs()
+    bad = err > 5e-5 * absref + 1e-6
+    assert not bool(bad.any()), f"{int(bad.sum())} of {bad.numel()} outside tolerance, max err {float(err.max())}"

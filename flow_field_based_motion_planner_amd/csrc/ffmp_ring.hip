@@ -177,7 +177,8 @@ size_t va_align(size_t bytes, size_t gran) {
   return a;
 }
 
-// a fresh piece mapped at its home address; on failure nothing stays allocated
+// a fresh piece mapped at its home address; on failure no memory stays allocated (only the
+// address reservation of a failed mapping, see below)
 hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out) {
   hipMemAllocationProp prop = dev_prop(device);
   ffmp_piece p = {};
@@ -191,8 +192,9 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
     return e;
   }
   if ((e = map_rw(p.home, bytes, p.h, device)) != hipSuccess) {
+    // The reservation is kept (never freed): an address range that was mapped once must not be
+    // handed out again, or the runtime can resolve later accesses there to this allocation.
     (void)hipMemUnmap(p.home, bytes);
-    (void)hipMemAddressFree(p.home, bytes);
     (void)hipMemRelease(p.h);
     return e;
   }
@@ -201,6 +203,7 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
 }
 
 // GB/s of the two-stream store probe over `bytes` of piece home + scale x `bytes` of partner
+// (< 0: the probe did not complete)
 double pair_gbs(char* a, char* b, size_t bytes, int scale, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int64_t n16 = (int64_t)(bytes / 16);
   const unsigned blocks = (unsigned)((n16 + 4095) / 4096);
@@ -212,7 +215,7 @@ double pair_gbs(char* a, char* b, size_t bytes, int scale, hipStream_t s, hipEve
     else
       hipLaunchKernelGGL(pair_probe_kernel<1>, dim3(blocks), dim3(256), 0, s, (f32x4*)a, (f32x4*)b, n16);
     (void)hipEventRecord(e1, s);
-    if (hipEventSynchronize(e1) != hipSuccess) return 0.0;
+    if (hipEventSynchronize(e1) != hipSuccess) return -1.0;  // a fault: the caller fails loudly
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
     if (r > 0 && ms < best) best = ms;  // first launch warms up
@@ -345,6 +348,15 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
     pool_put(cand);
     return fail(FFMP_E_HIP, "ffmp_ring: stream/event creation failed");
   }
+  // on failure: the candidates AND the pieces already chosen for earlier positions go back to the pool
+  auto give_back = [&](size_t upto) {
+    for (size_t q = 0; q < upto; ++q)
+      if (need[q] && r->pieces[q].h) {
+        cand.push_back(r->pieces[q]);
+        r->pieces[q] = ffmp_piece{};
+      }
+    pool_put(cand);
+  };
   int todo = 0;
   for (char n : need) todo += n != 0;
   // fresh pieces beyond need are the price of pairing (capped under an HBM budget)
@@ -378,8 +390,11 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
         if ((e = new_piece(device, g.piece, g.gran, &p)) != hipSuccess) {
           (void)hipGetLastError();
           if (pick >= 0 || !cand.empty()) break;  // out of memory: settle for what there is
-          pool_put(cand);
-          return fail(FFMP_E_HIP, "ffmp_ring: hipMemCreate/map of a %zu-byte piece: %s", g.piece, hipGetErrorString(e));
+          give_back(pos);
+          size_t free_b = 0, total_b = 0;
+          (void)hipMemGetInfo(&free_b, &total_b);
+          return fail(FFMP_E_HIP, "ffmp_ring: hipMemCreate/map of a %zu-byte piece: %s (device free %zu of %zu B)",
+                      g.piece, hipGetErrorString(e), free_b, total_b);
         }
         ++fresh;
         cand.push_back(p);
@@ -393,6 +408,10 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
         break;
       }
       const double gbs = pair_gbs(cand[c].home, pb, pbytes, g.scale, s, e0, e1);
+      if (gbs < 0.0) {
+        give_back(pos);
+        return fail(FFMP_E_HIP, "ffmp_ring: pairing probe failed: %s", hipGetErrorString(hipGetLastError()));
+      }
       ++r->pieces_tested;
       ++here;
       if (gbs >= kPairFastGBs) found_fast = true;
@@ -413,7 +432,7 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
       if (here >= 12) break;  // bounded search: keep the best seen
     }
     if (pick < 0) {
-      pool_put(cand);
+      give_back(pos);
       return fail(FFMP_E_HIP, "ffmp_ring: no piece available");
     }
     if (test) {

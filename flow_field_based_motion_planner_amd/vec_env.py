@@ -257,6 +257,8 @@ class FFMPVec:
             specs = [sp for sp in specs if sp[0] != "frames"]
         return specs
 
+    NO_VMM = "has no virtual memory management"  # ffmp_ring_create's message (ffmp_ring.hip ring_geom)
+
     def _alloc_ring(self) -> bool:
         """The seamless frame ring (HIP VMM, virtual slot W aliasing slot 0), if requested and
         the device supports it; its slots are built to pair well with the potential plane the
@@ -270,12 +272,23 @@ class FFMPVec:
                 slot = N * G * G * self._fes
                 spare = self.hbm_budget - self._arena_used - self.frame_window * self._ring_stride(slot)
                 prev_extra = _abi.set_tuning(_abi.TUNE_RING_EXTRA, 1 + max(0, spare // self._ring_piece(slot)))
-            self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, bits=8 * self._fes,
-                                           partner=partner)
+            try:
+                self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, bits=8 * self._fes,
+                                               partner=partner)
+            except _abi.FFMPBackendError as e:
+                if self.NO_VMM in str(e):
+                    raise
+                # the ring's pieces come from outside torch's caching allocator: give its cached
+                # blocks back to the device and try once more
+                torch.cuda.empty_cache()
+                self._ring = _abi.SeamlessRing(self.device.index, (N, G, G), self.frame_window, bits=8 * self._fes,
+                                               partner=partner)
             self.frames = self._ring.tensor
             self.ring_meta = self._ring.info()
-        except _abi.FFMPBackendError:
-            if self._seamless_req:
+        except _abi.FFMPBackendError as e:
+            # only a device without virtual memory management falls back to the wrapping ring;
+            # any other failure (out of memory, a fault) is the caller's to see
+            if self._seamless_req or self.NO_VMM not in str(e):
                 raise
             self._seamless_req = False  # no VMM here: the wrapping ring from now on
             return False

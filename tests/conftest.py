@@ -21,6 +21,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libffmp on cuda:0)")
 
 
+# Tests whose GPU work runs in child processes, or that need most of the HBM free, go first: this
+# process parks the pieces of every frame ring it creates for reuse and never unmaps them
+# (DESIGN §4), so late in the session a child (or a placement retry) would find less free HBM than
+# bench.py does on a fresh box.
+EARLY_MODULES = ("test_gpu_timed_path", "test_gpu_distributed")
+EARLY_TESTS = ("test_partner_relocation_keeps_a_consistent_env",)
+
+
+def pytest_collection_modifyitems(config, items):
+    def rank(it):
+        if it.module.__name__.rsplit(".", 1)[-1] in EARLY_MODULES:
+            return 0
+        return 1 if it.name in EARLY_TESTS else 2
+    items.sort(key=rank)
+
+
 @pytest.fixture(scope="session")
 def golden():
     with open(os.path.join(GOLDEN, "ref_pinned.json")) as f:

@@ -8,7 +8,8 @@ launch kind the autotune may pick — >= W + 2 steps, so every physical slot inc
 is written and then read as the older frame — comparing ALL envs with the C oracle after the
 reset and every step (planes, record, flags, counters bit-exact).  It runs as its own process:
 the ring's pieces are never unmapped, and a child that exits hands its ~75 GB of HBM
-back before the next test.  The reference behaviour the ring replaces:
+back before the next test.  W = 8 is asked for explicitly: bench.py's automatic choice on a free GPU,
+which the parent's parked ring pieces could otherwise shrink.  The reference behaviour the ring replaces:
 /root/reference/src/train.py:474-486 (make_temporal_maps)."""
 import json
 import os
@@ -22,6 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(fmt: str) -> dict:
+    import torch
+    torch.cuda.empty_cache()  # this process's cached blocks back to the device for the child
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tests", "timed_path_check.py"), "--obs-format", fmt]
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -131,6 +131,7 @@ def main() -> int:
     ap.add_argument("--envs", type=int, default=32768)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--seed", type=int, default=33)
+    ap.add_argument("--frame-window", type=int, default=8, help="bench.py's W (its automatic choice on a free GPU)")
     args = ap.parse_args()
     fmt, n = args.obs_format, args.envs
     t0 = time.time()
@@ -139,7 +140,7 @@ def main() -> int:
         print(f"[{time.time() - t0:6.1f}s] {msg}", file=sys.stderr, flush=True)
 
     cfg = preset("C3", max_steps=6, seed=args.seed)
-    env = FFMPVec(n, cfg, device="cuda:0", tuning=TUNING[fmt], obs_format=fmt)
+    env = FFMPVec(n, cfg, device="cuda:0", tuning=TUNING[fmt], obs_format=fmt, frame_window=args.frame_window)
     W = env.frame_window
     log(f"built {env!r}; ring {env.ring_meta}")
     if env.ring != "seamless" or W < 3:

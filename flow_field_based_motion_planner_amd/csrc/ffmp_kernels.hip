@@ -963,8 +963,15 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
 // env's whole plane from the record it just wrote.  The env step's float64 work of one block
 // overlaps the store streams of the other blocks on the CU, instead of running as its own
 // launch before the raster (~4 % of a C3 step).
+// Compact CT4 without flow planes: held to 7 waves per SIMD (72 VGPRs), the stand-alone CT4
+// raster's occupancy, which the compact store streams need (profiles/r02_occupancy.txt); the env
+// phase then keeps 20 B/lane of scratch, the same as the stand-alone env kernel.  Otherwise the
+// env phase's registers (89) would leave the raster 5 waves per SIMD.
+template <bool FLOW, int FMT>
+constexpr int kFusedMinWaves = (FMT == FMT_CT4 && !FLOW) ? 7 : 1;
+
 template <bool NT, bool XCD, bool FLOW, int FMT>
-__global__ __launch_bounds__(256) void step_raster_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+__global__ __launch_bounds__(256, (kFusedMinWaves<FLOW, FMT>)) void step_raster_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                           const int64_t* __restrict__ action, ffmp_state_t st,
                                                           ffmp_obs_t ob, ffmp_out_t out, int64_t sm_stride,
                                                           int64_t sm_frame, int32_t newest_only,

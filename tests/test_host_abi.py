@@ -164,7 +164,7 @@ def test_bench_traffic_lookup():
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     prof = os.path.join(os.path.dirname(HEADER), "..", "profiles")
-    for name, fused, fmt in (("C3", False, "f32"), ("C3", True, "f32"), ("C3", False, "u8f16")):
+    for name, fused, fmt in (("C3", False, "f32"), ("C3", True, "f32"), ("C3", False, "u8f16"), ("C3", True, "u8f16")):
         label = name + ("" if fmt == "f32" else "_" + fmt) + ("_fused" if fused else "")
         path = os.path.join(prof, f"pmc_traffic_{label}.json")
         if not os.path.exists(path):

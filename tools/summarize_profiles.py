@@ -9,7 +9,7 @@
                                           raster: mean over the pass's timed launches (the frame
                                           window mixes full and newest-only launches), other
                                           kernels: median over dispatches
-  profiles/pmc_traffic_<cfg>.json         what bench.py reads for roofline.traffic
+  profiles/pmc_traffic_<cfg>[_fused].json what bench.py reads for roofline.traffic
 """
 import csv
 import glob
@@ -98,7 +98,9 @@ def main():
         if "raster_kernel" in pm["kernels"]:
             hb = pm["kernels"]["raster_kernel"]["hbm_bytes"]
             pm["raster_traffic_over_algorithmic"] = hb / alg
-            with open(os.path.join(OUT, f"pmc_traffic_{cfg}.json"), "w") as f:
+            # bench.py looks the one-launch step up under its own label first
+            sfx = "_fused" if pm["fused"] else ""
+            with open(os.path.join(OUT, f"pmc_traffic_{cfg}{sfx}.json"), "w") as f:
                 json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
                            "obs_format": bj["config"].get("obs_format", "f32"),
                            "raster_hbm_bytes_per_launch": hb,

@@ -46,19 +46,24 @@ def main():
     ap.add_argument("--no-mfma", action="store_true",
                     help="with --amp: conv2-conv4 through MIOpen instead of the MFMA kernel (conv_mfma.py)")
     ap.add_argument("--channels-last", action="store_true", help="NHWC Q-networks (Brain(channels_last=True))")
-    ap.add_argument("--input-channels", type=int, default=2, choices=[1, 2, 3],
-                    help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy")
+    ap.add_argument("--input-channels", type=int, default=2,
+                    help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy; "
+                         "with --temporal-maps: that many frames")
+    ap.add_argument("--temporal-maps", action="store_true",
+                    help="make_temporal_maps over --input-channels mono frames (train.py:474-486), from the frame ring")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
 
     dev = torch.device("cuda:0")
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed,
-                     flow=args.input_channels == 3)
-    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format)
+                     flow=args.input_channels == 3 and not args.temporal_maps)
+    window = max(args.input_channels, 3) if args.temporal_maps else None
+    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format, frame_window=window)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
                   mfma=False if args.no_mfma else None,
-                  channels_last=args.channels_last, input_channels=args.input_channels)
+                  channels_last=args.channels_last, input_channels=args.input_channels,
+                  temporal_maps=args.temporal_maps)
     obs = env.reset()
     tracker = EpisodeTracker(args.envs, device=dev)
     losses, updates = [], 0
@@ -89,6 +94,7 @@ def main():
     summ = tracker.summary()
     out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "warmup_seconds": t_warm - t0,
            "envs": args.envs, "steps": args.steps, "amp": args.amp, "mfma": bool(brain.mfma and args.amp), "channels_last": args.channels_last,
+           "input_channels": args.input_channels, "temporal_maps": args.temporal_maps,
            "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],
            "replay_bytes": brain.memory.hbm_bytes(), "replay_len": len(brain.memory), **summ}
     print(json.dumps(out))

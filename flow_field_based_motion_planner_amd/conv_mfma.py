@@ -141,7 +141,8 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 def fold_supported(conv: torch.nn.Conv2d) -> bool:
     c = conv.in_channels
     return (conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1
-            and c in (1, 2, 4) and conv.kernel_size[1] % (32 // c) == 0 and conv.out_channels in (32, 64))
+            and c in (1, 2, 3, 4) and conv.kernel_size[1] % (32 // (4 if c == 3 else c)) == 0
+            and conv.out_channels in (32, 64))
 
 
 def fold_input(x: torch.Tensor, F: int) -> torch.Tensor:
@@ -198,4 +199,8 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
 
 def fold_conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """relu(conv(x)) for a few-channel conv (the reference's conv1) through the MFMA kernel."""
-    return MFMAFoldConv2dReLU.apply(x, conv.weight, conv.bias)
+    w = conv.weight
+    if x.shape[1] == 3:  # a zero 4th channel (zero products) keeps the fold at F = 8 columns
+        x = torch.nn.functional.pad(x, (0, 0, 0, 0, 0, 1))
+        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 1))
+    return MFMAFoldConv2dReLU.apply(x, w, conv.bias)

@@ -1220,6 +1220,42 @@ void launch_env_lpe(int mode, int lpe, const ffmp_cfg_t& cfg, int64_t n, int64_t
 }
 
 // ============================================================================
+// make_temporal_maps over k frames (ffmp_temporal_maps, src/train.py:474-486): out[e][c] is the
+// frame of lag d = k-1-c, clamped to the episode start (min(d, since[e]): on is_first the
+// reference refills map_memory with the first frame).  A pure HBM copy, k planes read and
+// written per env: a block moves 16 KiB of one output plane, 16-B loads and stores.
+// ============================================================================
+struct LagOffsets {
+  int64_t b[FFMP_MAX_SERIES];  // byte offset of lag d's frame of env 0 from `frames`
+};
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void temporal_maps_kernel(const char* __restrict__ frames, LagOffsets lag,
+                                                            int32_t k, int64_t env_b, int64_t plane_b,
+                                                            const int32_t* __restrict__ since, int32_t chunks,
+                                                            char* __restrict__ out) {
+  const int64_t pc = blockIdx.x / chunks;  // output plane (e, c)
+  const int chunk = (int)(blockIdx.x - pc * chunks);
+  const int64_t e = pc / k;
+  const int c = (int)(pc - e * k);
+  int d = k - 1 - c;
+  if (since) d = min(d, max(since[e], 0));
+  d = __builtin_amdgcn_readfirstlane(d);  // block-uniform: the offset comes from the kernel arguments
+  const u32x4_t* src = reinterpret_cast<const u32x4_t*>(frames + lag.b[d] + e * env_b);
+  u32x4_t* dst = reinterpret_cast<u32x4_t*>(out + pc * plane_b);
+  const int64_t n16 = plane_b / 16;
+  const int64_t i0 = (int64_t)chunk * 1024 + threadIdx.x;
+  u32x4_t v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (i0 + 256 * u < n16) v[u] = __builtin_nontemporal_load(src + i0 + 256 * u);
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (i0 + 256 * u < n16) dst[i0 + 256 * u] = v[u];
+}
+
+// ============================================================================
 // C ABI
 // ============================================================================
 namespace {
@@ -1590,6 +1626,31 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
   hipLaunchKernelGGL(episode_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      n, *out, window, max_steps, threshold, flags, *ep);
   return check_launch("ffmp_episode_update");
+}
+
+int ffmp_temporal_maps(int64_t n, const void* frames, const int64_t* lag_offset, int32_t k, int64_t env_stride,
+                       int64_t plane, int32_t elem_bytes, const int32_t* since, void* out, void* stream) {
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (k < 1 || k > FFMP_MAX_SERIES) return fail(FFMP_E_ARG, "k must be in [1, %d], got %d", FFMP_MAX_SERIES, k);
+  if (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4)
+    return fail(FFMP_E_ARG, "elem_bytes must be 1, 2 or 4, got %d", elem_bytes);
+  if (plane <= 0 || env_stride < 0) return fail(FFMP_E_ARG, "plane must be > 0 and env_stride >= 0");
+  if (n == 0) return FFMP_OK;
+  if (!frames || !lag_offset || !out) return fail(FFMP_E_ARG, "frames/lag_offset/out is NULL");
+  const int64_t plane_b = plane * elem_bytes, env_b = env_stride * elem_bytes;
+  if (plane_b % 16 || env_b % 16 || ((uintptr_t)frames % 16) || ((uintptr_t)out % 16))
+    return fail(FFMP_E_ARG, "frames, out, the plane (%lld B) and env stride (%lld B) must be 16-byte aligned",
+                (long long)plane_b, (long long)env_b);
+  LagOffsets lag;
+  for (int d = 0; d < FFMP_MAX_SERIES; ++d) {
+    lag.b[d] = lag_offset[std::min(d, k - 1)] * elem_bytes;
+    if (lag.b[d] % 16) return fail(FFMP_E_ARG, "lag offset %d is not 16-byte aligned", d);
+  }
+  const int64_t chunks = (plane_b / 16 + 1023) / 1024;
+  if (n * k * chunks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many blocks for one launch");
+  hipLaunchKernelGGL(temporal_maps_kernel, dim3((unsigned)(n * k * chunks)), dim3(256), 0, (hipStream_t)stream,
+                     (const char*)frames, lag, k, env_b, plane_b, since, (int32_t)chunks, (char*)out);
+  return check_launch("ffmp_temporal_maps");
 }
 
 #ifdef FFMP_TRACE

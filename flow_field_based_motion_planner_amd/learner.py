@@ -15,7 +15,11 @@ are re-rastered there, and the Q-networks run on the batch without host round tr
   Brain.update_target_q_network (:430-431)      -> same
 
 input_channels (train.py:66-69): 2 (default, the configuration train.py runs) = [older, newest];
-1 = the newest frame; 3 = the newest frame + the env's flow planes (network.map_channels).
+1 = the newest frame; 3 = the newest frame + the env's flow planes (network.map_channels), as the
+option comments describe them.  temporal_maps=True instead takes make_temporal_maps' code path for
+a mono BEV image (train.py:474-486: map_memory holds INPUT_CHANNELS frames): input_channels = k
+frames, oldest first, served from the env's frame ring (FFMPVec.temporal_maps, k <= frame_window)
+and re-rastered by the replay memory (ReplayMemory(series=k)).
 
 amp=True (not the reference's arithmetic, opt-in): the Q-network forwards (acting, replay and
 target) run under torch.autocast bfloat16 — the convolutions on the MFMA units in bf16, fp32
@@ -45,7 +49,7 @@ class Brain:
     def __init__(self, env, capacity: int = CAPACITY, batch_size: int = BATCH_SIZE, gamma: float = GAMMA,
                  lr: float = LEARNING_RATE, replay_coupling: str = "reference", mask_terminal: bool = False,
                  seed: int = 0, amp: bool = False, channels_last: bool = False,
-                 input_channels: int = INPUT_CHANNELS, mfma: Optional[bool] = None):
+                 input_channels: int = INPUT_CHANNELS, mfma: Optional[bool] = None, temporal_maps: bool = False):
         self.env = env
         self.device = env.device
         self.num_actions = NUM_ACTIONS
@@ -57,11 +61,17 @@ class Brain:
         # map input per train.py:66-69 (network.map_channels): 2 = [older, newest] (default), 1 =
         # newest frame, 3 = newest frame + flow xy (needs the env's flow planes)
         self.input_channels = int(input_channels)
-        if self.input_channels == 3 and not env.cfg.flow:
-            raise ValueError("input_channels=3 needs an env with FFMPConfig(flow=True)")
-        if self.input_channels not in (1, 2, 3):
-            raise ValueError("input_channels must be 1, 2 or 3")
-        self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed)
+        self.temporal_maps = bool(temporal_maps)
+        if self.temporal_maps:
+            if not 1 <= self.input_channels <= env.frame_window:
+                raise ValueError(f"temporal_maps: input_channels must be in [1, frame_window={env.frame_window}]")
+        else:
+            if self.input_channels == 3 and not env.cfg.flow:
+                raise ValueError("input_channels=3 needs an env with FFMPConfig(flow=True)")
+            if self.input_channels not in (1, 2, 3):
+                raise ValueError("input_channels must be 1, 2 or 3")
+        series = self.input_channels if self.temporal_maps else 2
+        self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed, series=series)
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
             torch.manual_seed(seed)
@@ -77,7 +87,10 @@ class Brain:
         self.gen.manual_seed(int(seed) + 1)
 
     def _q(self, net: Network, coupling: str, sm, sg, sv, st, flow=None):
-        sm = map_channels(sm, flow, self.input_channels)  # uint8 frames (u8f16 layout) -> float 0 / 255
+        if self.temporal_maps:  # already the k frames
+            sm = sm.float() if sm.dtype == torch.uint8 else sm
+        else:
+            sm = map_channels(sm, flow, self.input_channels)  # uint8 frames (u8f16 layout) -> float 0 / 255
         if self.channels_last:
             sm = sm.contiguous(memory_format=torch.channels_last)
         prev, net.coupling = net.coupling, coupling
@@ -88,8 +101,11 @@ class Brain:
             net.coupling = prev
 
     def decide_action(self, obs: Dict[str, torch.Tensor], episode: torch.Tensor) -> torch.Tensor:
-        """Epsilon-greedy actions (N,) int64 for every env (train.py:337-349)."""
+        """Epsilon-greedy actions (N,) int64 for every env (train.py:337-349).  With temporal_maps
+        the map input is the env's k-frame series (FFMPVec.temporal_maps), not obs["state_m"]."""
         n = obs["state_m"].shape[0]
+        if self.temporal_maps:
+            obs = dict(obs, state_m=self.env.temporal_maps(self.input_channels))
         epsilon = 0.5 * (1.0 / (episode.to(torch.float64) + 1.0))
         u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
         self.main_q_network.eval()

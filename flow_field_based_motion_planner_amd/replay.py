@@ -21,6 +21,14 @@ state_m / observe_m the env emitted (the raster is a pure function of the record
 
 Transitions are causal: (obs_t, a_t, obs_t+1, r_t+1).  (The reference's asynchronous ROS loop
 pairs the action chosen from obs_t-1 with obs_t; a synchronous env has no such skew.)
+
+series=k > 2 (make_temporal_maps over k mono frames, train.py:66-69, 474-486; FFMPVec.temporal_maps):
+a transition also keeps the records of the k-2 steps before its state and the state's steps since
+reset; sample() rasters the k frames of each side, the lag-d frame being the newest frame of the
+record d steps back, clamped to the episode start (the last frame is the older frame of the record
+k-2 steps back: k-1 raster launches write k frames per sample).  The memory keeps the k-2 previous
+records of every env itself (push_begin must see every step); a transition pushed less than k-2
+steps after the memory was created sees its deepest lags clamped to the oldest record it has.
 """
 from __future__ import annotations
 
@@ -43,7 +51,7 @@ class ReplayMemory:
     sample() materialises the map stacks with the env's raster kernel (state_m / observe_m
     f32 (B,2,G,G); with `potential=True` also the potential planes (B,G,G) of both sides)."""
 
-    def __init__(self, env, capacity: int, seed: int = 0):
+    def __init__(self, env, capacity: int, seed: int = 0, series: int = 2):
         if not getattr(env, "keep_terminal", False):
             raise ValueError("ReplayMemory needs FFMPVec(..., keep_terminal=True) (terminal records of done envs)")
         if capacity < env.num_envs:
@@ -59,6 +67,16 @@ class ReplayMemory:
         self.action = torch.zeros(self.capacity, dtype=torch.int64, device=dev)
         self.reward = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.done = torch.zeros(self.capacity, dtype=torch.bool, device=dev)
+        self.series = int(series)
+        if not 1 <= self.series <= _abi.MAX_SERIES:
+            raise ValueError(f"series must be in [1, {_abi.MAX_SERIES}]")
+        H = max(self.series - 2, 0)
+        # series > 2: records r_t-1 .. r_t-k+2 of the state, its steps since reset, and every env's
+        # last k-2 records (newest first; `_seen` steps of them are real)
+        self.s_hist = torch.zeros(self.capacity, H, R, dtype=torch.float32, device=dev) if H else None
+        self.s_since = torch.zeros(self.capacity, dtype=torch.int32, device=dev) if H else None
+        self._env_hist = torch.zeros(H, env.num_envs, R, dtype=torch.float32, device=dev) if H else None
+        self._seen = 0
         self.index = 0   # next slot (train.py:216)
         self.size = 0    # len(self.memory)
         self._pending = None
@@ -70,9 +88,12 @@ class ReplayMemory:
     def __len__(self) -> int:
         return self.size
 
+    def _tensors(self):
+        return [t for t in (self.s_record, self.o_record, self.s_small, self.o_small, self.action, self.reward,
+                            self.done, self.s_hist, self.s_since, self._env_hist) if t is not None]
+
     def hbm_bytes(self) -> int:
-        return sum(t.numel() * t.element_size() for t in (self.s_record, self.o_record, self.s_small, self.o_small,
-                                                           self.action, self.reward, self.done))
+        return sum(t.numel() * t.element_size() for t in self._tensors())
 
     # ----------------------------------------------------------------- push
     def _slots(self, n: int):
@@ -86,9 +107,18 @@ class ReplayMemory:
         env = env or self.env
         n = env.num_envs
         small = torch.cat([env.state_g, env.state_v, env.state_t], dim=1)
+        H = self.series - 2
+        if H > 0:
+            since = env.t.clamp(max=self._seen)
         for dst, src, cnt in self._slots(n):
             self.s_record[dst:dst + cnt].copy_(env.record[src:src + cnt])
             self.s_small[dst:dst + cnt].copy_(small[src:src + cnt])
+            if H > 0:
+                self.s_hist[dst:dst + cnt].copy_(self._env_hist[:, src:src + cnt].transpose(0, 1))
+                self.s_since[dst:dst + cnt].copy_(since[src:src + cnt])
+        if H > 0:  # the next step's history: this state's record first
+            self._env_hist.copy_(torch.cat((env.record.unsqueeze(0), self._env_hist[:H - 1])))
+            self._seen = min(self._seen + 1, H)
         self._pending = n
 
     def push_end(self, action: torch.Tensor, env=None) -> None:
@@ -114,19 +144,42 @@ class ReplayMemory:
         G = self.cfg.grid
         want = (B, potential)
         if self._bufs.get(key, (None,))[0] != want:
-            sm = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device)
+            sm = torch.empty(B, max(self.series, 2), G, G, dtype=torch.float32, device=self.device)
             pot = torch.empty(B, G, G, dtype=torch.float32, device=self.device) if potential else None
             flow = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device) if self.cfg.flow else None
             self._bufs[key] = (want, sm, pot, flow)
         return self._bufs[key][1:]
 
-    def _raster(self, records: torch.Tensor, sm, pot, flow) -> None:
-        ob = _abi.ObsT(sm.data_ptr(), None, None, None, pot.data_ptr() if pot is not None else None, None, None,
+    def _raster(self, records: torch.Tensor, sm, pot, flow, pos: int = 0, newest_only: bool = False) -> None:
+        """Raster `records` into sm[:, pos] (older) and sm[:, pos + 1] (newest); newest_only: the
+        older frame only for reset records (FFMP_RASTER_NEWEST)."""
+        G2 = self.cfg.grid * self.cfg.grid
+        ob = _abi.ObsT(sm.data_ptr() + pos * G2 * sm.element_size(), None, None, None,
+                       pot.data_ptr() if pot is not None else None, None, None,
                        flow.data_ptr() if flow is not None else None)
+        ob.state_m_stride, ob.state_m_frame_stride = sm.shape[1] * G2, G2
+        cpb, flags = self.env.raster_shape
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         with torch.cuda.device(self.device):
             _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), records.shape[0], records.data_ptr(), None,
-                                               C.byref(ob), *self.env.raster_shape, stream), "ffmp_raster")
+                                               C.byref(ob), cpb, flags | (_abi.RASTER_NEWEST if newest_only else 0),
+                                               stream), "ffmp_raster")
+
+    def _raster_series(self, recs: torch.Tensor, since: torch.Tensor, sm, pot, flow) -> None:
+        """k frames per sample from recs (B, k-1, R) = records r_t, r_t-1, ..., r_t-k+2: the lag-d
+        frame (d <= k-2) is the newest frame of r_t-min(d, since), the lag-(k-1) frame the older
+        frame of r_t-min(k-2, since) (a reset record's older frame is its newest).  Frames two
+        launches both write carry the same values."""
+        k = self.series
+        B = recs.shape[0]
+        ar = torch.arange(B, device=self.device)
+        for d in range(k - 1):
+            j = since.to(torch.int64).clamp(max=d)
+            rec = recs[ar, j].contiguous()
+            full = d == k - 2
+            # the potential / flow planes belong to the newest frame only (d = 0)
+            self._raster(rec, sm, pot if d == 0 else None, flow if d == 0 else None, pos=k - 2 - d,
+                         newest_only=not full)
 
     def sample_indices(self, batch_size: int, replacement: bool = False) -> torch.Tensor:
         if batch_size > self.size and not replacement:
@@ -146,8 +199,18 @@ class ReplayMemory:
         o_rec = self.o_record.index_select(0, idx)
         s_sm, s_pot, s_flow = self._batch_planes("s", B, potential)
         o_sm, o_pot, o_flow = self._batch_planes("o", B, potential)
-        self._raster(s_rec, s_sm, s_pot, s_flow)
-        self._raster(o_rec, o_sm, o_pot, o_flow)
+        if self.series > 2:
+            hist = self.s_hist.index_select(0, idx)
+            s_since = self.s_since.index_select(0, idx)
+            s_recs = torch.cat((s_rec.unsqueeze(1), hist), 1)                          # r_t .. r_t-k+2
+            o_recs = torch.cat((o_rec.unsqueeze(1), s_rec.unsqueeze(1), hist[:, :-1]), 1)  # r_t+1 .. r_t-k+3
+            self._raster_series(s_recs, s_since, s_sm, s_pot, s_flow)
+            self._raster_series(o_recs, s_since + 1, o_sm, o_pot, o_flow)
+        else:
+            self._raster(s_rec, s_sm, s_pot, s_flow)
+            self._raster(o_rec, o_sm, o_pot, o_flow)
+            if self.series == 1:  # the newest frame only (a view)
+                s_sm, o_sm = s_sm[:, 1:], o_sm[:, 1:]
         ss = self.s_small.index_select(0, idx)
         os_ = self.o_small.index_select(0, idx)
         tr = Transition(s_sm, ss[:, 0:2], ss[:, 2:4], ss[:, 4:5], self.action.index_select(0, idx).view(B, 1),
@@ -159,12 +222,17 @@ class ReplayMemory:
             extra["flow"], extra["observe_flow"] = s_flow, o_flow
         return tr, extra
 
+    _SD = ("s_record", "o_record", "s_small", "o_small", "action", "reward", "done", "s_hist", "s_since", "_env_hist")
+
     def state_dict(self) -> dict:
-        return {"s_record": self.s_record.clone(), "o_record": self.o_record.clone(), "s_small": self.s_small.clone(),
-                "o_small": self.o_small.clone(), "action": self.action.clone(), "reward": self.reward.clone(),
-                "done": self.done.clone(), "index": self.index, "size": self.size}
+        sd = {k: getattr(self, k).clone() for k in self._SD if getattr(self, k) is not None}
+        sd.update(index=self.index, size=self.size, series=self.series, seen=self._seen)
+        return sd
 
     def load_state_dict(self, sd: dict) -> None:
-        for k in ("s_record", "o_record", "s_small", "o_small", "action", "reward", "done"):
-            getattr(self, k).copy_(sd[k])
-        self.index, self.size = int(sd["index"]), int(sd["size"])
+        if int(sd.get("series", 2)) != self.series:
+            raise ValueError(f"state_dict of a series={sd.get('series', 2)} memory, this one has {self.series}")
+        for k in self._SD:
+            if getattr(self, k) is not None:
+                getattr(self, k).copy_(sd[k])
+        self.index, self.size, self._seen = int(sd["index"]), int(sd["size"]), int(sd.get("seen", 0))

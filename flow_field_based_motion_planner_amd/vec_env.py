@@ -133,6 +133,11 @@ class FFMPVec:
         self._fused_req = fused
         self.fused_flags = _abi.RASTER_NT
         self._wpos = 0  # frame slot of state_m[:, 0]
+        # temporal_maps(k): physical ring slots of the newest frames, newest first (lag 0, 1, ...),
+        # and whether every env's lags beyond them are clamped away (a full reset) or unknown
+        # (a checkpoint reload re-rasters only the [older, newest] pair)
+        self._hist = []
+        self._hist_from_reset = False
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
         if pipeline is None:
@@ -847,6 +852,66 @@ class FFMPVec:
             wrap = p == W - 1 and not self.WRAP_VIA_ALIAS
             self._obs_c.state_m_frame_stride = -(W - 1) * fs if wrap else fs
 
+    def _note_window(self, full: bool) -> None:
+        """Frame history after a raster at the current window: the newest frame's slot first;
+        a full raster also rewrote the older slot (with the previous newest frame)."""
+        if self.frame_window == 2:
+            return
+        W = self.frame_window
+        new, old = (self._wpos + 1) % W, self._wpos % W
+        prev = self._hist
+        if full:
+            self._hist = [new, old] + [s for s in prev[1:] if s not in (new, old)]
+        else:
+            self._hist = [new] + [s for s in prev if s != new]
+        del self._hist[W:]
+        if len(self._hist) < len(prev) + 1:
+            # a frame of the history was overwritten: lags beyond the list are no longer
+            # guaranteed to be clamped away
+            self._hist_from_reset = False
+
+    def temporal_maps(self, k: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """make_temporal_maps (src/train.py:474-486) over the last k frames: (N, k, G, G), oldest
+        first, each env's lags clamped to its episode start (is_first refills the reference's
+        map_memory with the first frame) — the reference's INPUT_CHANNELS = k with a mono BEV
+        image (train.py:66-69).  k <= 2: a view of state_m.  k > 2: gathered from the frame ring
+        (k <= frame_window) by ffmp_temporal_maps into `out` (or a new tensor)."""
+        self._check_open()
+        k = int(k)
+        if k < 1:
+            raise ValueError("k must be >= 1")
+        if k <= 2 and out is None:
+            return self.state_m[:, 2 - k:]
+        if k > self.frame_window or k > _abi.MAX_SERIES:
+            raise ValueError(f"temporal_maps({k}) needs frame_window >= {k} (this env keeps {self.frame_window}; "
+                             f"at most {_abi.MAX_SERIES})")
+        if self._needs_reset:
+            raise RuntimeError("call reset() before temporal_maps()")
+        N, G = self.num_envs, self.cfg.grid
+        if self.frame_window == 2:
+            lag_slots = None
+            offs = [G * G, 0]  # contiguous (N, 2, G, G): newest, older
+            env_stride = 2 * G * G
+        else:
+            if len(self._hist) < k and not self._hist_from_reset:
+                raise RuntimeError(f"the frame ring holds {len(self._hist)} known frames since the last reload; "
+                                   f"temporal_maps({k}) needs {k} (step {k - len(self._hist)} more times, or reset())")
+            # lags the ring has not seen since a full reset are never read (every env's lag is
+            # clamped to its steps since that reset): any valid slot stands in
+            lag_slots = [self._hist[min(d, len(self._hist) - 1)] for d in range(k)]
+            offs = [s * self.frames.stride(0) for s in lag_slots]
+            env_stride = G * G
+        offs = (offs + [offs[-1]] * k)[:k]
+        if out is None:
+            out = torch.empty(N, k, G, G, dtype=self.frames.dtype, device=self.device)
+        elif out.shape != (N, k, G, G) or out.dtype != self.frames.dtype or not out.is_contiguous() \
+                or out.device != self.device:
+            raise ValueError(f"out must be a contiguous {self.frames.dtype} tensor of shape {(N, k, G, G)} on {self.device}")
+        lag = (C.c_int64 * k)(*offs)
+        _abi.check(self.lib.ffmp_temporal_maps(N, self.frames.data_ptr(), lag, k, env_stride, G * G, self._fes,
+                                               self.t.data_ptr(), out.data_ptr(), self._stream()), "ffmp_temporal_maps")
+        return out
+
     def _raster_bytes(self, n: int, full: bool) -> int:
         """Algorithmic bytes of one raster launch over n envs (excluding the older frames of envs
         reset during a newest-only launch: one frame each, added by bench.py from the episode counts)."""
@@ -901,6 +966,8 @@ class FFMPVec:
             s = self._stream()
             if mask is None:
                 self._set_window(0)
+                self._hist, self._hist_from_reset = [], True
+                self._note_window(True)
             _abi.check(self.lib.ffmp_reset(C.byref(self._cfg_c), self.num_envs, self.env_offset, _ptr(m), initial,
                                            C.byref(self._state_c), C.byref(self._obs_c), s), "ffmp_reset")
             self._raster_launch(True, m)
@@ -942,6 +1009,7 @@ class FFMPVec:
         else:
             full = p > self.frame_window - 2
         self._set_window(0 if full else p)
+        self._note_window(full)
         return full
 
     def _state_bytes(self, n: int) -> int:
@@ -1151,6 +1219,8 @@ class FFMPVec:
             self.cfg = self.cfg.replace(seed=seed)
             self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
         self.raster()
+        self._hist, self._hist_from_reset = [], False  # older frames than the pair are not restored
+        self._note_window(True)
         self._needs_reset = False
 
     def hbm_bytes(self) -> int:

@@ -20,6 +20,8 @@
  *                          rewarder2 (src/gym_ffmp/envs/ffmp.py:179-188) in-GPU
  *   ffmp_ring_*, ffmp_dlpack -> storage of make_temporal_maps' 2-frame stack
  *                          (src/train.py:474-486) kept in place (optional helper)
+ *   ffmp_temporal_maps  -> make_temporal_maps over INPUT_CHANNELS = k mono frames
+ *                          (src/train.py:66-69, 474-486) served from the frame ring
  *   ffmp_raster         -> external /bev_flow_estimator + /temporal_bev_publisher
  *                          (src/train.py:116-121, make_temporal_maps :474-486)
  *   ffmp_reward_done    -> FFMP.rewarder / rewarder2 / reward_calculator /
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 4
+#define FFMP_ABI_VERSION 5
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -350,6 +352,22 @@ int ffmp_episode_init(int64_t n, const uint8_t* mask, int32_t flags, ffmp_episod
  * out.truncated; reward unused).  max_steps = 0 when out.done already includes truncation. */
 int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_t max_steps,
                         double threshold, int32_t flags, ffmp_episode_t* ep, void* stream);
+
+/* make_temporal_maps (src/train.py:474-486) over k frames of the mono BEV image — the code path
+ * of the reference's INPUT_CHANNELS = k with one image channel: map_memory keeps the last k
+ * frames and is refilled with the first frame of an episode (is_first).  Served from a frame
+ * window (the seamless ring keeps W >= k frames in place):
+ *   out[e][c] = frame of lag d = k-1-c of env e (c = 0 oldest, k-1 newest), with the lag clamped
+ *               to min(d, since[e]) — since = steps since the env's reset (ffmp_state_t.t), or
+ *               NULL for no clamp;
+ *   the frame of lag d of env e is at frames + lag_offset[d] + e * env_stride (elements;
+ *   lag_offset a HOST array of k entries).
+ * elem_bytes 1 (uint8 frames), 2 or 4 (float32); plane = G*G elements; out (n, k, G, G)
+ * contiguous.  frames, out, plane * elem_bytes, env_stride * elem_bytes and every lag offset in
+ * bytes must be 16-byte aligned.  A pure copy: k planes read and k written per env. */
+#define FFMP_MAX_SERIES 16
+int ffmp_temporal_maps(int64_t n, const void* frames, const int64_t* lag_offset, int32_t k, int64_t env_stride,
+                       int64_t plane, int32_t elem_bytes, const int32_t* since, void* out, void* stream);
 
 /* Seamless frame ring — an optional allocation helper (the step / raster entry points above
  * still never allocate).  The temporal stack of make_temporal_maps (src/train.py:474-486)

@@ -129,16 +129,17 @@ def test_conv_dilated_matches_float64(B, H, W, KH, KW, dx, N):
     assert not bool(((y.double() - ref).abs() > 5e-5 * absref + 1e-6).any())
 
 
-@pytest.mark.parametrize("C", [2, 1])
+@pytest.mark.parametrize("C", [2, 1, 3])
 def test_folded_conv1_against_float64(C):
     """The reference Network's conv1 (C map channels -> 32, k = 32, 100^2 -> 69^2; train.py:234)
     with its kernel columns folded into 32 channels: forward vs float64 of the same bf16 operands
     (then ReLU, bf16), weight / bias gradients vs float64 autograd of the masked product."""
-    from flow_field_based_motion_planner_amd.conv_mfma import MFMAFoldConv2dReLU
+    from flow_field_based_motion_planner_amd.conv_mfma import fold_conv_relu, fold_supported
     g = torch.Generator(device=DEV).manual_seed(5 + C)
     conv = torch.nn.Conv2d(C, 32, kernel_size=32).to(DEV)
+    assert fold_supported(conv)
     x = (torch.rand((3, C, 100, 100), device=DEV, generator=g) > 0.85).float() * 255
-    y = MFMAFoldConv2dReLU.apply(x, conv.weight, conv.bias)
+    y = fold_conv_relu(conv, x)  # C = 3: a zero fourth channel
     x64 = x.double()
     w64 = conv.weight.detach().to(torch.bfloat16).double().requires_grad_(True)
     b64 = conv.bias.detach().double().requires_grad_(True)

@@ -143,3 +143,37 @@ def test_replay_with_other_input_channels(channels):
     torch.testing.assert_close(loss, ref_loss.detach(), rtol=1e-5, atol=1e-5)
     a = brain.decide_action(env.obs, torch.zeros(32, dtype=torch.int32, device=DEV))
     assert a.shape == (32,) and int(a.max()) < 28
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_temporal_maps_input(amp):
+    """Brain(temporal_maps=True, input_channels=3): make_temporal_maps' code path for a mono BEV
+    image (train.py:474-486, INPUT_CHANNELS frames): acting on env.temporal_maps(3), replaying
+    3-frame series; one update equals the restated reference arithmetic on the sampled series
+    (amp: the MFMA path, conv1's 3 channels folded with a zero fourth, within bf16 bounds)."""
+    cfg = FFMPConfig(grid=100, n_obst=4, n_beams=64, moving=True, max_steps=6, seed=33)
+    env = FFMPVec(32, cfg, device=DEV, keep_terminal=True, frame_window=4)
+    env.reset()
+    brain = Brain(env, capacity=256, batch_size=48, seed=6, input_channels=3, temporal_maps=True, amp=amp)
+    assert brain.main_q_network.conv1.in_channels == 3 and brain.memory.series == 3
+    _fill(brain, env, 4)
+    idx = torch.randperm(len(brain.memory), device=DEV)[:48]
+    main0 = copy.deepcopy(brain.main_q_network)
+    targ0 = copy.deepcopy(brain.target_q_network)
+    b, ex = brain.memory.sample(48, index=idx)
+    assert b.state_m.shape == (48, 3, 100, 100)
+    b = type(b)(*[t.clone() for t in b])
+    loss = brain.replay(index=idx)
+    main0.eval()
+    targ0.eval()
+    with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=amp):
+        sav = main0(b.state_m, b.state_g, b.state_v, b.state_t).float().gather(1, b.action)
+        a_m = main0(b.observe_m, b.observe_g, b.observe_v, b.observe_t).float().detach().max(1)[1].view(-1, 1)
+        nxt = targ0(b.observe_m, b.observe_g, b.observe_v, b.observe_t).float().gather(1, a_m).detach().squeeze()
+    ref_loss = nn.MSELoss()(sav, (b.reward + 0.95 * nxt).unsqueeze(1))
+    tol = 2e-2 if amp else 1e-5
+    torch.testing.assert_close(loss, ref_loss.detach(), rtol=tol, atol=tol)
+    a = brain.decide_action(env.obs, torch.zeros(32, dtype=torch.int32, device=DEV))
+    assert a.shape == (32,) and int(a.max()) < 28
+    with pytest.raises(ValueError):
+        Brain(env, capacity=256, input_channels=5, temporal_maps=True)  # more frames than the window

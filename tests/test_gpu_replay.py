@@ -122,3 +122,46 @@ def test_ring_semantics_and_sampling():
         ReplayMemory(FFMPVec(N, cfg, device=DEV), capacity=cap)  # needs keep_terminal
     with pytest.raises(RuntimeError):
         mem.push_end(torch.zeros(N, dtype=torch.int64, device=DEV))
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_series_sample_reproduces_temporal_maps(k):
+    """ReplayMemory(series=k): the k-frame state series re-rastered from the stored records equals
+    env.temporal_maps(k) before the step; the observation series equals it after the step, or for
+    an env that reset, the state series slid by one with the terminal frame appended (the reference
+    appends the observed frame to map_memory; is_first refills it only on the next iteration)."""
+    cfg = FFMPConfig(grid=64, n_obst=12, n_beams=32, moving=True, max_steps=5, obst_rmax=0.5, obst_vmax=1.2,
+                     world_half=2.4, goal_min=0.6, goal_max=1.5, seed=23)
+    N, T = 32, 11
+    env = FFMPVec(N, cfg, device=DEV, keep_terminal=True, frame_window=k + 1)
+    mem = ReplayMemory(env, capacity=N * T, series=k)
+    env.reset()
+    rng = np.random.default_rng(2)
+    before, after, term, dones = [], [], [], []
+    for _ in range(T):
+        before.append(env.temporal_maps(k).clone())
+        mem.push_begin()
+        a = torch.as_tensor(rng.integers(0, 28, N), device=DEV)
+        env.step(a)
+        mem.push_end(a)
+        after.append(env.temporal_maps(k).clone())
+        term.append(env.term_record.clone())
+        dones.append(env.done.clone())
+    done_all = torch.cat(dones)
+    assert 0 < int(done_all.sum()) < N * T
+    tr, ex = mem.sample(0, index=torch.arange(N * T, device=DEV), potential=True)
+    assert tr.state_m.shape == (N * T, k, 64, 64)
+    s_want = torch.cat(before)
+    assert torch.equal(tr.state_m, s_want)
+    nd = ~done_all
+    assert torch.equal(tr.observe_m[nd], torch.cat(after)[nd])
+    assert torch.equal(tr.observe_m[done_all][:, :-1], s_want[done_all][:, 1:])
+    oc = Cfg.from_config(cfg)
+    recs = torch.cat(term)[done_all].cpu().numpy()
+    newest = raster(oc, Record.unpack(recs, cfg.n_obst), False)[0][:, 1]
+    assert np.array_equal(tr.observe_m[done_all][:, -1].cpu().numpy(), newest)
+    sd = mem.state_dict()
+    mem2 = ReplayMemory(env, capacity=N * T, series=k)
+    mem2.load_state_dict(sd)
+    tr2, _ = mem2.sample(0, index=torch.arange(N * T, device=DEV))
+    assert torch.equal(tr2.state_m, tr.state_m) and torch.equal(tr2.observe_m, tr.observe_m)

@@ -24,6 +24,7 @@
 // workgroup) come from global memory through L1/L2 into registers, one tap ahead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -51,11 +52,29 @@ __device__ __forceinline__ void load_row_regs(const char* __restrict__ src, int 
   }
 }
 
+// LDS images of NHWC rows are padded by 16 bytes after every 256: column col starts at
+// cell_off(col) = col * C * 2 + (col / (256 / (C * 2))) * 16.  The A fragment of lane r reads one
+// 16-byte chunk of column xcol + r; unpadded, the columns of a ds_read_b128 lane group (C * 2 bytes
+// apart) fall on 2 (C = 64) or 4 (C = 32) of the 16 bank quads — 8- / 4-way conflicts; padded, the
+// 16 lanes {0-3, 12-15, 20-27} of a group take 16 distinct quads, and the chunk offsets stay
+// compile-time constants (no per-read address arithmetic, unlike an XOR swizzle).
+template <int C>
+__host__ __device__ __forceinline__ int cell_off(int col) {
+  constexpr int CPR = 256 / (C * 2);  // columns per 256 bytes
+  return col * C * 2 + (col / CPR) * 16;
+}
+template <int C>
+__host__ __device__ __forceinline__ int lds_pitch(int W) {  // bytes of one padded row image
+  return cell_off<C>(W - 1) + C * 2;
+}
+
+template <int C>
 __device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4 (&buf)[4]) {
+  constexpr int CPC = C / 8;  // 16-byte chunks per column
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = threadIdx.x + 256 * i;
-    if (q < chunks) *(uint4*)(dst + 16 * q) = buf[i];
+    if (q < chunks) *(uint4*)(dst + cell_off<C>(q / CPC) + 16 * (q % CPC)) = buf[i];
   }
 }
 
@@ -82,8 +101,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   const int p0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int rowbytes = W * C * 2;      // one tensor row = one ring slot
+  const int rowbytes = W * C * 2;      // one tensor row
+  const int pitch = lds_pitch<C>(W);   // its padded image = one ring slot
   const int chunks = rowbytes / 16;    // <= 4 * 256 (host check)
+  const int zero_off = RING * pitch;   // a zero column (PAD: reads outside the tensor's columns)
   const int yf = p0 / Wo;
   const int yl = min(P - 1, p0 + PT - 1) / Wo;
   const char* xb = (const char*)x + (size_t)b * H * rowbytes;
@@ -111,8 +132,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   for (int row = yf + ky_lo; row <= yl + ky_lo; ++row) {
     uint4 buf[4];
     load_row_regs<C>(row_src(row), chunks, buf);
-    store_row_lds(lds + (row % RING) * rowbytes, chunks, buf);
+    store_row_lds<C>(lds + (row % RING) * pitch, chunks, buf);
   }
+  if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
 
   f32x16 acc[MBW][NB];
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
     if (ky >= wk_lo && ky <= wk_hi) {
       int aoff[MBW];
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * rowbytes + h * 16;
+      for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
       for (int kx = 0; kx < KW; ++kx) {
         // the next tap: (ky, kx + 1), else (ky + 1, 0) while the wave has rows left (the last
         // tap re-reads its own)
@@ -151,22 +173,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
 #pragma unroll
           for (int s = 0; s < C / 16; ++s)
             bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
-        int coff[MBW];
-        bool cok[MBW];
+        // the lane's column of each block, or the zero column outside the tensor (PAD)
+        int abase[MBW];
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb) {
           const int col = xcol[mb] + kx * dx;
-          cok[mb] = !PAD || (unsigned)col < (unsigned)W;
-          coff[mb] = (PAD ? min(max(col, 0), W - 1) : col) * C * 2;
+          abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + h * 16;
         }
 #pragma unroll
         for (int s = 0; s < C / 16; ++s) {
           bf16x8 a[MBW];
 #pragma unroll
-          for (int mb = 0; mb < MBW; ++mb) {
-            a[mb] = *(const bf16x8*)(lds + aoff[mb] + coff[mb] + s * 32);
-            if (PAD && !cok[mb]) a[mb] = bf16x8{};
-          }
+          for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * 32);
 #pragma unroll
           for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
@@ -179,7 +197,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
           for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
       }
     }
-    if (more) store_row_lds(lds + ((yl + ky + 1) % RING) * rowbytes, chunks, nrow);
+    if (more) store_row_lds<C>(lds + ((yl + ky + 1) % RING) * pitch, chunks, nrow);
     __syncthreads();
   }
 
@@ -228,20 +246,23 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int rowbytes = W * C * 2;
+  const int pitch = lds_pitch<C>(W);  // padded row images (cell_off)
   const int chunks = rowbytes / 16;
   const int yf = p0 / Wo;
   const int yl = min(P - 1, p0 + PT - 1) / Wo;
   const char* xb = (const char*)x + (size_t)b * H * rowbytes;
   const int ky_lo = max(0, pad - yl), ky_hi = min(KH - 1, pad + H - 1 - yf);
+  const int zero_off = (yl + ky_hi - yf - ky_lo + 1) * pitch;  // a zero column after the window
 
   // the window: logical rows [yf + ky_lo, yl + ky_hi], slot = row - yf - ky_lo
   for (int row = yf + ky_lo; row <= yl + ky_hi; ++row) {
     const int real = row - pad;
     const char* src = (real >= 0 && real < H) ? xb + (size_t)real * rowbytes : nullptr;
     for (int q = threadIdx.x; q < chunks; q += 256)
-      *(uint4*)(lds + (row - yf - ky_lo) * rowbytes + 16 * q) =
+      *(uint4*)(lds + (row - yf - ky_lo) * pitch + cell_off<C>(q / (C / 8)) + 16 * (q % (C / 8))) =
           src ? *(const uint4*)(src + 16 * (size_t)q) : uint4{0u, 0u, 0u, 0u};
   }
+  if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
   int ypos[MBW], xcol[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
@@ -260,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
   for (int ky = ky_lo + wave; ky <= ky_hi; ky += kWaves) {
     int aoff[MBW];
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb) aoff[mb] = (ypos[mb] + ky) * rowbytes + h * 16;
+    for (int mb = 0; mb < MBW; ++mb) aoff[mb] = (ypos[mb] + ky) * pitch;
     bf16x8 bcur[NB][C / 16];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
@@ -275,22 +296,17 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
 #pragma unroll
         for (int s = 0; s < C / 16; ++s)
           bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
-      int coff[MBW];
-      bool cok[MBW];
+      int abase[MBW];
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
         const int col = xcol[mb] + kx * dx;
-        cok[mb] = !PAD || (unsigned)col < (unsigned)W;
-        coff[mb] = (PAD ? min(max(col, 0), W - 1) : col) * C * 2;
+        abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + h * 16;
       }
 #pragma unroll
       for (int s = 0; s < C / 16; ++s) {
         bf16x8 a[MBW];
 #pragma unroll
-        for (int mb = 0; mb < MBW; ++mb) {
-          a[mb] = *(const bf16x8*)(lds + aoff[mb] + coff[mb] + s * 32);
-          if (PAD && !cok[mb]) a[mb] = bf16x8{};
-        }
+        for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * 32);
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
@@ -336,7 +352,8 @@ constexpr size_t kSmallRedBytes = 4 * 4 * 16 * 64 * sizeof(float);  // conv_smal
 
 // LDS bytes of conv_small_kernel's window for this shape (a 128-position tile's rows + KH - 1)
 size_t small_window_bytes(int Wo, int KH, int W, int C) {
-  return (size_t)((128 + Wo - 1) / Wo + 1 + KH - 1) * W * C * 2;
+  const int pitch = C == 64 ? lds_pitch<64>(W) : lds_pitch<32>(W);
+  return (size_t)((128 + Wo - 1) / Wo + 1 + KH - 1) * pitch + C * 2;  // + the zero column
 }
 
 template <int C, int NB, bool PAD>
@@ -356,6 +373,12 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
 // fragment) whose rounding of an image's positions costs at most 10 % more than the tightest, and
 // whose ring leaves room for two workgroups per CU
 int pick_mbw(int P, int Wo, size_t slotbytes) {
+  static const int forced = [] {  // FFMP_CONV_MBW = 1 / 2 / 4: a probe knob (tools/conv_variants.py)
+    const char* v = getenv("FFMP_CONV_MBW");
+    const int m = v ? atoi(v) : 0;
+    return (m == 1 || m == 2 || m == 4) ? m : 0;
+  }();
+  if (forced) return forced;
   long padded[3], least = -1;
   const int mbws[3] = {4, 2, 1};
   for (int i = 0; i < 3; ++i) {
@@ -378,7 +401,7 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   constexpr int PT = kWaves * MBW * 32;
   const int span = (PT + Wo - 1) / Wo + 1;  // input rows a tile reads for one ky
   const int ring = span + 1;                // + the row loaded for the next ky
-  const size_t lds = (size_t)ring * W * C * 2;
+  const size_t lds = (size_t)ring * lds_pitch<C>(W) + C * 2;  // + the zero column
   if (lds > 160 * 1024)
     return fail(FFMP_E_ARG, "ffmp_conv2d: a ring of %d input rows (%zu bytes) exceeds the 160 KiB LDS", ring, lds);
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
@@ -395,9 +418,9 @@ int launch_fwd(const void* x, const void* w, const float* bias, void* y, int B, 
                int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   // small images with a kernel deep enough to split over the waves: conv_small_kernel
-  if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= kSmallRedBytes && (W * C * 2) % 16 == 0)
+  if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= 76 * 1024 && (W * C * 2) % 16 == 0)
     return launch_small<C, NB, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-  switch (pick_mbw(Ho * Wo, Wo, (size_t)W * C * 2)) {
+  switch (pick_mbw(Ho * Wo, Wo, (size_t)lds_pitch<C>(W))) {
     case 4: return launch_fwd_mbw<C, NB, 4, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     case 2: return launch_fwd_mbw<C, NB, 2, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     default: return launch_fwd_mbw<C, NB, 1, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);

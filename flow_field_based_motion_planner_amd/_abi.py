@@ -204,6 +204,7 @@ RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
 RASTER_TILE2, RASTER_TILE4, RASTER_TILE8 = 16, 32, 64
 RASTER_NARROW = 128  # FFMP_OBS_U8F16: 4 cells per lane instead of 16
 RASTER_TILE16 = 256
+RASTER_MID8 = 512  # FFMP_OBS_U8F16: 8 cells per lane
 
 
 def set_tuning(key: int, value: int) -> int:

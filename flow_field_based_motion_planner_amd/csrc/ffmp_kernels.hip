@@ -518,6 +518,15 @@ FFMP_DEV void store16_u8(uint8_t* p, const float occ[16]) {
   else *reinterpret_cast<u32x4*>(p) = v;
 }
 
+// 8 cells of a lane as one 8-B frame store
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+FFMP_DEV void store8_u8(uint8_t* p, const float occ[8]) {
+  u32x2 v = {pack4_u8(occ), pack4_u8(occ + 4)};
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+  else *reinterpret_cast<u32x2*>(p) = v;
+}
+
 template <bool NT>
 FFMP_DEV void store8_h(_Float16* p, const float* U) {
   f16x8 v = {(_Float16)U[0], (_Float16)U[1], (_Float16)U[2], (_Float16)U[3],
@@ -581,7 +590,14 @@ FFMP_DEV int64_t logical_block() {
 // FFMP_OBS_U8F16, 4 cells per lane) or FMT_CT16 (compact, 16 cells per lane: a wave task is
 // 1024 cells, so the per-task cull / wall / index work is spread over 4x the cells — the compact
 // raster writes 3 bytes per cell and is bound by that per-task work, not by HBM; needs G % 16 == 0).
-constexpr int FMT_F32 = 0, FMT_CT4 = 1, FMT_CT16 = 2;
+// FMT_CT8 (FFMP_RASTER_MID8, G % 8 == 0): 8 cells per lane, an 8-B frame store and a 16-B potential
+// store per lane (512-cell wave tasks).
+constexpr int FMT_F32 = 0, FMT_CT4 = 1, FMT_CT16 = 2, FMT_CT8 = 3;
+// The CT8 raster is held to 6 waves per SIMD (84 VGPRs instead of the compiler's 112 at 4): C3
+// newest-only raster 0.985-1.025 -> 0.954-0.956 ms (profiles/r03b_ct8_shapes.txt).
+#ifndef FFMP_CT8_MIN_WAVES
+#define FFMP_CT8_MIN_WAVES 6
+#endif
 
 // The raster of cells [tile * cells_per_block, ...) of env e by the whole 256-thread block
 // (block-uniform arguments; contains a block barrier).  Compact formats: state_m holds uint8
@@ -597,7 +613,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
                                                         int32_t tile_log2r, float4* s_cur, float4* s_prev,
                                                         float2* s_vel, float* s_hdr) {
   constexpr bool CT = FMT != FMT_F32;
-  constexpr int CPL = FMT == FMT_CT16 ? 16 : 4;  // cells per lane in a wave task
+  constexpr int CPL = FMT == FMT_CT16 ? 16 : FMT == FMT_CT8 ? 8 : 4;  // cells per lane in a wave task
   constexpr int WC = 64 * CPL;                   // cells per wave task
   const int K = cfg.n_obst;
   const int G = cfg.grid;
@@ -623,7 +639,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
   // 11 VGPRs — 108 -> 72 VGPRs, 4 -> 7 waves per SIMD, compact C3 raster 1.15-1.29 -> 1.00-1.13 ms
   // (profiles/r02_occupancy.txt).  Not for the float32 layout (store-bound: 7 waves per SIMD ran
   // its steps ~2 % slower than 4) nor for FMT_CT16 (the scheduler then took 188 VGPRs, not 167).
-  auto hv = [&](int i) { return FMT == FMT_CT4 ? uni(s_hdr[i]) : s_hdr[i]; };
+  auto hv = [&](int i) { return (FMT == FMT_CT4 || FMT == FMT_CT8) ? uni(s_hdr[i]) : s_hdr[i]; };
   const FrameHdr hc{hv(0), hv(1), hv(2), hv(3)};
   const FrameHdr hp{hv(4), hv(5), hv(6), hv(7)};
   const float gx = hv(8), gy = hv(9);
@@ -729,6 +745,16 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
         store8_h<NT>(h0 + q + 8, fx + 8 % CPL);
         store8_h<NT>(h0 + G2 + q, fy);
         store8_h<NT>(h0 + G2 + q + 8, fy + 8 % CPL);
+      }
+      return;
+    }
+    if constexpr (CT && CPL == 8) {
+      if (write_old) store8_u8<NT>(b0 + q, occp);
+      store8_u8<NT>(b1 + q, occc);
+      if (hp16) store8_h<NT>(hp16 + q, U);
+      if (FLOW) {
+        store8_h<NT>(h0 + q, fx);
+        store8_h<NT>(h0 + G2 + q, fy);
       }
       return;
     }
@@ -856,7 +882,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
               }
             }
           }
-          if (FMT == FMT_CT16) {
+          if constexpr (FMT == FMT_CT16) {
             if (write_old) store16_w<NT>(b0 + q, wp);
             store16_w<NT>(b1 + q, wc);
             if (hp16) {
@@ -879,7 +905,27 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
               store8_h<NT>(h0 + G2 + q, fy);
               store8_h<NT>(h0 + G2 + q + 8, fy + 8 % CPL);
             }
-          } else if (FMT == FMT_CT4) {
+          } else if constexpr (FMT == FMT_CT8) {
+            const u32x2 fw = {wc[0], wc[NW - 1]}, pw = {wp[0], wp[NW - 1]};
+            if (NT) {
+              if (write_old) __builtin_nontemporal_store(pw, reinterpret_cast<u32x2*>(b0 + q));
+              __builtin_nontemporal_store(fw, reinterpret_cast<u32x2*>(b1 + q));
+            } else {
+              if (write_old) *reinterpret_cast<u32x2*>(b0 + q) = pw;
+              *reinterpret_cast<u32x2*>(b1 + q) = fw;
+            }
+            if (hp16) {
+              const f16x8 u8v = {(_Float16)U2[0].x, (_Float16)U2[0].y, (_Float16)U2[1 % NP].x, (_Float16)U2[1 % NP].y,
+                                 (_Float16)U2[2 % NP].x, (_Float16)U2[2 % NP].y, (_Float16)U2[3 % NP].x,
+                                 (_Float16)U2[3 % NP].y};
+              if (NT) __builtin_nontemporal_store(u8v, reinterpret_cast<f16x8*>(hp16 + q));
+              else *reinterpret_cast<f16x8*>(hp16 + q) = u8v;
+            }
+            if (FLOW) {
+              store8_h<NT>(h0 + q, fx);
+              store8_h<NT>(h0 + G2 + q, fy);
+            }
+          } else if constexpr (FMT == FMT_CT4) {
             if (NT) {
               if (write_old) __builtin_nontemporal_store(wp[0], reinterpret_cast<uint32_t*>(b0 + q));
               __builtin_nontemporal_store(wc[0], reinterpret_cast<uint32_t*>(b1 + q));
@@ -934,7 +980,7 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
 }
 
 template <bool NT, bool XCD, bool FLOW, int FMT>
-__global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
+__global__ __launch_bounds__(256, (FMT == FMT_CT8 && !FLOW ? FFMP_CT8_MIN_WAVES : 1)) void raster_kernel(ffmp_cfg_t cfg, int64_t n, int32_t bpe,
                                                      int32_t cells_per_block,
                                                      const float* __restrict__ record,
                                                      const uint8_t* __restrict__ mask,
@@ -968,7 +1014,7 @@ __global__ __launch_bounds__(256) void raster_kernel(ffmp_cfg_t cfg, int64_t n, 
 // phase then keeps 20 B/lane of scratch, the same as the stand-alone env kernel.  Otherwise the
 // env phase's registers (89) would leave the raster 5 waves per SIMD.
 template <bool FLOW, int FMT>
-constexpr int kFusedMinWaves = (FMT == FMT_CT4 && !FLOW) ? 7 : 1;
+constexpr int kFusedMinWaves = (FMT == FMT_CT4 && !FLOW) ? 7 : (FMT == FMT_CT8 && !FLOW) ? FFMP_CT8_MIN_WAVES : 1;
 
 template <bool NT, bool XCD, bool FLOW, int FMT>
 __global__ __launch_bounds__(256, (kFusedMinWaves<FLOW, FMT>)) void step_raster_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
@@ -1270,7 +1316,9 @@ int32_t tile_rows_log2(int32_t flags) {
 // lane's 16 cells stay in one row (G % 16 == 0) unless FFMP_RASTER_NARROW asks for 4.
 int raster_format(bool compact, int grid, int32_t flags) {
   if (!compact) return FMT_F32;
-  return (grid % 16 == 0 && !(flags & FFMP_RASTER_NARROW)) ? FMT_CT16 : FMT_CT4;
+  if (flags & FFMP_RASTER_NARROW) return FMT_CT4;
+  if ((flags & FFMP_RASTER_MID8) && grid % 8 == 0) return FMT_CT8;
+  return grid % 16 == 0 ? FMT_CT16 : FMT_CT4;
 }
 
 // Calls f(NT, XCD, FLOW, FMT) with std::integral_constant arguments for the runtime choice (the
@@ -1283,6 +1331,9 @@ void dispatch_variant(int fmt, bool nt, bool xcd, bool fl, F&& f) {
     if (fmt == FMT_CT16) {
       if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_CT16>{});
       else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT16>{});
+    } else if (fmt == FMT_CT8) {
+      if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_CT8>{});
+      else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT8>{});
     } else if (fmt == FMT_CT4) {
       if (fl) f(NT_, XCD_, T{}, std::integral_constant<int, FMT_CT4>{});
       else f(NT_, XCD_, N{}, std::integral_constant<int, FMT_CT4>{});
@@ -1465,7 +1516,7 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record, const 
   // 2-D wave tiles: R rows x (cells per wave task)/R columns, where the plane and the block split into them
   int32_t tile_log2r = tile_rows_log2(flags);
   if (tile_log2r) {
-    const int C = (fmt == FMT_CT16 ? 1024 : 256) >> tile_log2r, R = 1 << tile_log2r;
+    const int C = (fmt == FMT_CT16 ? 1024 : fmt == FMT_CT8 ? 512 : 256) >> tile_log2r, R = 1 << tile_log2r;
     const bool whole_bands = cpb >= G2 || (cpb % (cfg->grid * R)) == 0;
     if ((cfg->grid % C) != 0 || !whole_bands) tile_log2r = 0;  // the 1-D chunks (identical results)
   }
@@ -1538,7 +1589,7 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
   const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
   const int fmt = raster_format(ct, cfg->grid, flags);
   int32_t tile_log2r = tile_rows_log2(flags);
-  if (tile_log2r && (cfg->grid % ((fmt == FMT_CT16 ? 1024 : 256) >> tile_log2r)) != 0)
+  if (tile_log2r && (cfg->grid % ((fmt == FMT_CT16 ? 1024 : fmt == FMT_CT8 ? 512 : 256) >> tile_log2r)) != 0)
     tile_log2r = 0;  // a block is one whole plane
   const dim3 grid((unsigned)n), block(256);
   hipStream_t s = (hipStream_t)stream;

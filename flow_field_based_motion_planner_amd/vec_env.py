@@ -703,12 +703,20 @@ class FFMPVec:
         (32768, _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW),
         (65536, _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW),
         (32768, _abi.RASTER_NT | _abi.RASTER_NARROW),
+        # round 3: 8 cells per lane (an 8-B frame and a 16-B potential store per lane), 4 x 128-cell
+        # tiles, 6 waves per SIMD: 0.954-0.985 ms against the 4-cell tiles' 1.00-1.03 at C3
+        # (profiles/r03b_ct8_shapes.txt)
+        (65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8),
+        (32768, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8),
+        (65536, _abi.RASTER_NT | _abi.RASTER_TILE8 | _abi.RASTER_MID8),
+        (65536, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4 | _abi.RASTER_MID8),
     )
     COMPACT_FUSED_FLAGS = (
         _abi.RASTER_NT | _abi.RASTER_TILE16, _abi.RASTER_NT | _abi.RASTER_TILE8, _abi.RASTER_NT | _abi.RASTER_TILE4,
         _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW, _abi.RASTER_PLAIN | _abi.RASTER_TILE16,
         _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE16, _abi.RASTER_NT,
         _abi.RASTER_NT | _abi.RASTER_TILE2 | _abi.RASTER_NARROW,
+        _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8,
     )
 
     XCD_SHAPES = True  # autotune candidates include the XCD-aware block remap

@@ -237,6 +237,9 @@ int ffmp_raster(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                                 R x 1024/R cells and need G % (1024/R) == 0 */
 #define FFMP_RASTER_TILE16 256 /* 16 x 16-cell tile (compact 16 cells per lane: 16 x 64) */
 #define FFMP_RASTER_NARROW 128 /* FFMP_OBS_U8F16: keep 4 cells per lane (256-cell wave tasks) */
+#define FFMP_RASTER_MID8 512   /* FFMP_OBS_U8F16, G % 8 == 0: 8 cells per lane (512-cell wave tasks: an
+                                  8-B frame and a 16-B potential store per lane; tiles R x 512/R);
+                                  NARROW wins when both are set */
 int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
                    const uint8_t* mask, ffmp_obs_t* obs, int32_t cells_per_block,
                    int32_t flags, void* stream);

@@ -12,9 +12,12 @@ from flow_field_based_motion_planner_amd.config import PRESETS  # noqa: E402
 from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 
 NT, PL, XCD = _abi.RASTER_NT, _abi.RASTER_PLAIN, _abi.RASTER_XCD
-T4, T8, T16, NAR = _abi.RASTER_TILE4, _abi.RASTER_TILE8, _abi.RASTER_TILE16, _abi.RASTER_NARROW
-SHAPES = [(16384, NT | T4 | NAR), (32768, NT | T16), (65536, NT | T16), (65536, PL | T16), (32768, PL | T16),
-          (65536, NT | XCD | T16), (65536, NT | T8), (65536, NT | T4), (32768, NT | T4 | NAR), (65536, NT | T4 | NAR)]
+T2, T4, T8, T16, NAR = _abi.RASTER_TILE2, _abi.RASTER_TILE4, _abi.RASTER_TILE8, _abi.RASTER_TILE16, _abi.RASTER_NARROW
+M8 = _abi.RASTER_MID8
+SHAPES = [(65536, NT | T4 | NAR), (65536, NT | T2 | NAR),
+          # round 3: 8 cells per lane (FFMP_RASTER_MID8)
+          (65536, NT | T4 | M8), (32768, NT | T4 | M8), (65536, NT | XCD | T4 | M8), (65536, PL | T4 | M8),
+          (16384, NT | T4 | M8), (65536, NT | T8 | M8)]
 
 
 def main():

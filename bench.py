@@ -239,6 +239,39 @@ def time_compact(FFMPVec, name, cfg, n, dev, steps, warmup, seed):
     return out
 
 
+def time_compact_child(name, steps, seed):
+    """The compact-layout leg in a child process of its own (bench.py --obs-format u8f16), as a user
+    running that layout would: this process has parked its float32 rings' pieces (never unmapped,
+    DESIGN §4), and a compact ring built here would draw them first.  None if the child fails."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", name, "--obs-format", "u8f16", "--strong-config",
+           "none", "--cpu-seconds", "0", "--compact-steps", "0", "--steps", str(steps), "--warmup", "10",
+           "--seed", str(seed)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    except subprocess.TimeoutExpired:
+        print("warning: compact-layout child timed out", file=sys.stderr)
+        return None
+    line = next((ln for ln in reversed(r.stdout.splitlines()) if ln.startswith("{")), None)
+    if r.returncode != 0 or line is None:
+        print(f"warning: compact-layout child failed (rc {r.returncode}): {r.stderr[-2000:]}", file=sys.stderr)
+        return None
+    d = json.loads(line)
+    rl, a = d["roofline"], d.get("raster_autotune", {})
+    ring = a.get("ring") or {}
+    return {"obs_format": "u8f16", "value": d["value"], "unit": "env-steps/s", "steps": d["steps"],
+            "ms_per_step": d["ms_per_step"], "step_ms_events": d["step_ms_events"], "kernel": rl["kernel"],
+            "kernel_ms": rl["kernel_ms"], "achieved_gbs": rl["achieved"], "frac": rl["frac"],
+            "algorithmic_bytes_per_launch": rl["algorithmic_bytes_per_launch"], "traffic": rl.get("traffic"),
+            "frame_window": d["config"]["frame_window"], "ring": d["config"]["ring"], "fused": d["config"]["fused"],
+            "shape": a.get("shape_newest"), "construct_s": d.get("construct_s"), "hbm_bytes": d.get("hbm_bytes"),
+            "ring_pairing": {k: ring.get(k) for k in ("pieces", "pair_probes", "pair_gbs_min", "pair_gbs_max",
+                                                      "partner_tries", "rebuilds", "reverts")},
+            "process": "a child process of its own (bench.py --obs-format u8f16)"}
+
+
 def _gather_floats(vals, world, dev, backend):
     """Every rank's `vals` (list of floats) -> (world, len) list of lists; one collective."""
     import torch
@@ -396,6 +429,17 @@ def main():
     _release(env)
     env = None
 
+    # the compact layout (N = 1), before the strong leg: that one's ring takes most of the HBM, and
+    # the pieces of rings this process dropped stay mapped
+    compact = None
+    if world == 1 and args.obs_format == "f32" and args.compact_steps > 0 and not args.tuning \
+            and not args.no_potential and not args.flow:
+        torch.cuda.empty_cache()
+        compact = time_compact_child(name, args.compact_steps, args.seed)
+        if compact is None:  # in this process instead (after the float32 instance: placement-dependent)
+            compact = time_compact(FFMPVec, name, cfg, n, dev, args.compact_steps, 10, args.seed)
+            compact["process"] = "this process, after the float32 instance"
+
     # second leg: the strong-scaling preset split over the ranks (C4's 65,536 envs over
     # 1, 2, 4, 8 GPUs), so one driver command yields both curves
     strong_leg = None
@@ -411,11 +455,6 @@ def main():
             env = None
             strong_leg.pop("raster_autotune", None)
             strong_leg.pop("per_launch_envs", None)
-
-    compact = None
-    if world == 1 and args.obs_format == "f32" and args.compact_steps > 0 and not args.tuning \
-            and not args.no_potential and not args.flow:
-        compact = time_compact(FFMPVec, name, cfg, n, dev, args.compact_steps, 10, args.seed)
 
     if rank == 0:
         rl = dict(leg["roofline"], traffic=traffic)

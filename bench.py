@@ -293,6 +293,11 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     from flow_field_based_motion_planner_amd.config import bytes_per_env_step
     from flow_field_based_motion_planner_amd.vec_env import FFMPVec
     fb = 4 if args.obs_format == "f32" else 1
+    # the actions first: the first use of torch's random kernels loads their code (a GPU-idle gap),
+    # and after an idle gap the raster runs slow for ~10 steps while the clocks ramp back up
+    # (profiles/r03b_transient*.txt) — here that gap falls before construction, not before the warm-up
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank + (0 if main_leg else 5000))
+    actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
     torch.cuda.synchronize(dev)
     t_c = time.perf_counter()
     env = FFMPVec(n, cfg, device=dev, env_offset=offset, potential=not args.no_potential, pipeline=args.pipeline,
@@ -306,8 +311,11 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         with open(args.save_tuning, "w") as f:
             json.dump(env.tuning(), f)
     free, total = torch.cuda.mem_get_info(dev)
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank + (0 if main_leg else 5000))
-    actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
+    # the torch kernel the loop's bookkeeping uses (episode.sum) is loaded now: its first call loads
+    # its code with the GPU idle, and after such a gap the raster runs slow for ~10 steps while the
+    # clocks ramp back up (profiles/r03b_transient_loop.txt) — it must not fall between the warm-up
+    # and the timed steps
+    int(env.episode.sum())
     env.reset()
     for w in range(W):
         env.step(actions[w])
@@ -315,10 +323,10 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     # ~10 % of a C2 step); the dominant kernel keeps its per-launch pairs (roofline.achieved)
     ev_loop = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     raster_ev = []
+    ep0_t = env.episode.sum()  # read after the loop: no host round trip between the sync and the loop
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ep0 = int(env.episode.sum())
     t0 = time.perf_counter()
     ev_loop[0].record()
     for k in range(K):
@@ -329,7 +337,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         dist.barrier()
     el_local = time.perf_counter() - t0
     env.check_errors()
-    resets = int(env.episode.sum()) - ep0  # auto-resets in the timed steps
+    resets = int(env.episode.sum()) - int(ep0_t)  # auto-resets in the timed steps
     per_rank = _gather_floats([el_local, construct_s, float(n)], world, dev, args.dist_backend)
     el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
 

@@ -391,6 +391,10 @@ class FFMPVec:
         (16384, _abi.RASTER_NT | _abi.RASTER_TILE8), (4096, _abi.RASTER_PLAIN | _abi.RASTER_TILE4),
         # smaller tiled blocks for small planes (C2's 0.09 ms launches lose ~10 % to their last blocks)
         (4096, _abi.RASTER_NT | _abi.RASTER_TILE4), (2048, _abi.RASTER_NT | _abi.RASTER_TILE4),
+        # round 3: 4,096-cell tiled blocks with the XCD remap — at C3 the fastest shape in the step loop
+        # (2.265 ms against 2.345 without the remap and 2.39 for 8,192-cell blocks;
+        # profiles/r03b_transient_shapes.txt, steady state)
+        (4096, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4), (4096, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE2),
     )
 
     def _raster_gbs_steady(self, steps: int = 3) -> Dict[bool, Tuple[float, float]]:

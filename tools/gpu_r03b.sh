@@ -44,8 +44,8 @@ task_spec() {
       if [ $v = base ]; then L=$R/tools/_build/libffmp_base.so; else L=$R/flow_field_based_motion_planner_amd/lib/libffmp.so; fi
       FFMP_LIB=$L timeout -k 10 300 python3 $R/bench.py --steps 50 --warmup 10 --cpu-seconds 0 > $R/gpurun_out/ab/s_${v}_$rep.log 2>&1 || exit 1
       grep '^{' $R/gpurun_out/ab/s_${v}_$rep.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; c=d.get('compact_layout') or {}; f=d['raster_autotune'].get('fused', {})
-  print('$v', 'f32', round(d['value']/1e6,3), 'M', r['kernel'], round(r['kernel_ms'],4), 'fused', f.get('chosen'), f.get('recheck'), 'slots', d['raster_autotune'].get('ring', {}).get('repair', [{}])[-1].get('slot_ms'), '| compact', round(c.get('value', 0)/1e6,2), 'M', c.get('kernel'), round(c.get('kernel_ms', 0),4), c.get('fused'))" || exit 1
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; c=d.get('compact_layout') or {}; f=d['raster_autotune'].get('fused', {})
+print('$v', 'f32', round(d['value']/1e6,3), 'M', r['kernel'], round(r['kernel_ms'],4), 'fused', f.get('chosen'), f.get('recheck'), 'slots', d['raster_autotune'].get('ring', {}).get('repair', [{}])[-1].get('slot_ms'), '| compact', round(c.get('value', 0)/1e6,2), 'M', c.get('kernel'), round(c.get('kernel_ms', 0),4), c.get('fused'))" || exit 1
     done
   done
 }
@@ -81,8 +81,8 @@ task_ct8_check() {
   for i in 1 2; do
     timeout -k 10 400 python -u bench.py > gpurun_out/r03b_ct8_bench_$i.log 2>&1 || { tail -20 gpurun_out/r03b_ct8_bench_$i.log; exit 1; }
     tail -1 gpurun_out/r03b_ct8_bench_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']
-  print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), '| compact', round(c['value']/1e6,2), c['kernel'], round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], c['fused'])"
+import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']
+print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), '| compact', round(c['value']/1e6,2), c['kernel'], round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], c['fused'])"
   done
 }
 
@@ -90,24 +90,24 @@ task_compact_fresh() {
   for i in 1 2 3; do
     timeout -k 10 300 python -u bench.py --obs-format u8f16 --strong-config none --cpu-seconds 0 --steps 100 --warmup 10 > gpurun_out/r03b_compact_fresh_$i.log 2>&1 || { tail -20 gpurun_out/r03b_compact_fresh_$i.log; exit 1; }
     tail -1 gpurun_out/r03b_compact_fresh_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
-  print('u8f16', round(d['value']/1e6,2), 'M', r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), a.get('shape_newest'), a.get('fused', {}).get('chosen'), a.get('fused', {}).get('flags'), a.get('fused', {}).get('recheck'), {k: a.get('ring', {}).get(k) for k in ('pair_probes','pair_gbs_min','pair_gbs_max','partner_tries')})"
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
+print('u8f16', round(d['value']/1e6,2), 'M', r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), a.get('shape_newest'), a.get('fused', {}).get('chosen'), a.get('fused', {}).get('flags'), a.get('fused', {}).get('recheck'), {k: a.get('ring', {}).get(k) for k in ('pair_probes','pair_gbs_min','pair_gbs_max','partner_tries')})"
   done
 }
 
 task_bench() {
   timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r03b_bench_child.log 2>&1 || { tail -20 gpurun_out/r03b_bench_child.log; exit 1; }
   tail -1 gpurun_out/r03b_bench_child.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']; s=d.get('strong') or {}
-  print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), '| strong', round(s.get('value',0)/1e6,3), '| compact', round(c['value']/1e6,2), c['kernel'], round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], c['fused'], c.get('process'))"
+import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']; s=d.get('strong') or {}
+print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), '| strong', round(s.get('value',0)/1e6,3), '| compact', round(c['value']/1e6,2), c['kernel'], round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], c['fused'], c.get('process'))"
 }
 
 task_launches() {
   for i in 1 2 3; do
     timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --dump-launches --compact-steps 0 --strong-config none --cpu-seconds 0 > gpurun_out/r03b_launches_$i.log 2> gpurun_out/r03b_launches_$i.err || { tail -20 gpurun_out/r03b_launches_$i.err; exit 1; }
     tail -1 gpurun_out/r03b_launches_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
-  print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), 'fused', a['fused'].get('chosen'), a['fused'].get('recheck'), 'slots', a['ring']['repair'][-1]['slot_ms'])"
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
+print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), 'fused', a['fused'].get('chosen'), a['fused'].get('recheck'), 'slots', a['ring']['repair'][-1]['slot_ms'])"
     grep -v amdgpu.ids gpurun_out/r03b_launches_$i.err | tail -25 | tr '\n' ' '; echo
   done
 }
@@ -116,7 +116,7 @@ task_benchloop() {
   for i in 1 2 3; do
     timeout -k 10 400 python -u bench.py --steps 20 --warmup ${WARM:-5} --dump-launches --compact-steps 0 --strong-config none --cpu-seconds 0 --tuning tools/tuning_c3_4096x37.json > gpurun_out/r03b_loop_$i.log 2> gpurun_out/r03b_loop_$i.err || { tail -20 gpurun_out/r03b_loop_$i.err; exit 1; }
     tail -1 gpurun_out/r03b_loop_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4))"
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4))"
     grep "raster ms" gpurun_out/r03b_loop_$i.err
   done
 }
@@ -126,8 +126,8 @@ task_transient() {
   for i in 1 2; do
     timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --dump-launches --compact-steps 0 --strong-config none --cpu-seconds 0 > gpurun_out/r03b_settle_$i.log 2> gpurun_out/r03b_settle_$i.err || { tail -20 gpurun_out/r03b_settle_$i.err; exit 1; }
     tail -1 gpurun_out/r03b_settle_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
-  print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), 'fused', a['fused'].get('chosen'), a['fused'].get('recheck'), 'construct', d['construct_s'])"
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
+print(round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), 'fused', a['fused'].get('chosen'), a['fused'].get('recheck'), 'construct', d['construct_s'])"
     grep "raster ms" gpurun_out/r03b_settle_$i.err
   done
 }
@@ -150,8 +150,8 @@ task_final_bench() {
   for i in 1 2; do
     timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r03b_final_bench_$i.log 2>&1 || { tail -20 gpurun_out/r03b_final_bench_$i.log; exit 1; }
     tail -1 gpurun_out/r03b_final_bench_$i.log | python3 -c "
-  import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']; s=d.get('strong') or {}; b=d['cpu_baseline']
-  print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), d['raster_autotune']['shape_newest'], '| strong', round(s.get('value',0)/1e6,3), '| compact', round(c['value']/1e6,2), round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], '| cpu', round(b['value']/1e3,1), 'K')"
+import json,sys; d=json.loads(sys.stdin.read()); c=d['compact_layout']; r=d['roofline']; s=d.get('strong') or {}; b=d['cpu_baseline']
+print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), d['raster_autotune']['shape_newest'], '| strong', round(s.get('value',0)/1e6,3), '| compact', round(c['value']/1e6,2), round(c['kernel_ms'],4), round(c['frac'],3), c['shape'], '| cpu', round(b['value']/1e3,1), 'K')"
   done
 }
 

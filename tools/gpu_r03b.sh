@@ -16,6 +16,7 @@
 #   transient-shapes  round 3 (second session): the post-idle slow start by raster launch shape (tools/transient_shapes.py)
 #   transient-reset   round 3 (second session): slow start after reset(): episodes or GPU state (tools/transient_reset.py)
 #   full              round 3 (second session): the whole GPU suite as the driver runs it, then smoke()
+#   shape-sweep       steady-state raster time of launch shapes beyond the autotune's (tools/shape_sweep.py)
 #   final-bench       round 3 (second session): the driver's bench command line on the final code, two fresh processes
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -155,6 +156,10 @@ print('f32', round(d['value']/1e6,3), r['kernel'], round(r['kernel_ms'],4), roun
   done
 }
 
+task_shape_sweep() {
+  timeout -k 10 300 python3 tools/shape_sweep.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r03b_shape_sweep.txt
+}
+
 case "$1" in
   series) task_series ;;
   learner-prof) task_learner_prof ;;
@@ -172,5 +177,6 @@ case "$1" in
   transient-reset) task_transient_reset ;;
   full) task_full ;;
   final-bench) task_final_bench ;;
-  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench}"; exit 2 ;;
+  shape-sweep) task_shape_sweep ;;
+  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep}"; exit 2 ;;
 esac

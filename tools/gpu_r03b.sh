@@ -17,6 +17,7 @@
 #   transient-reset   round 3 (second session): slow start after reset(): episodes or GPU state (tools/transient_reset.py)
 #   full              round 3 (second session): the whole GPU suite as the driver runs it, then smoke()
 #   shape-sweep       steady-state raster time of launch shapes beyond the autotune's (tools/shape_sweep.py)
+#   configs           the other BASELINE configs' bench lines (C2, the C5 per-GPU share)
 #   final-bench       round 3 (second session): the driver's bench command line on the final code, two fresh processes
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -160,6 +161,15 @@ task_shape_sweep() {
   timeout -k 10 300 python3 tools/shape_sweep.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r03b_shape_sweep.txt
 }
 
+task_configs() {
+  for c in C2 C5; do
+    timeout -k 10 600 python -u bench.py --config $c --steps 50 --warmup 10 --compact-steps 0 --strong-config none --cpu-seconds 0 > gpurun_out/r03b_config_$c.log 2>&1 || { tail -20 gpurun_out/r03b_config_$c.log; exit 1; }
+    tail -1 gpurun_out/r03b_config_$c.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; a=d['raster_autotune']
+print('$c', round(d['value']/1e6,3), 'M', r['kernel'], round(r['kernel_ms'],4), round(r['frac'],3), a.get('shape_newest'), a.get('fused', {}).get('chosen'), round(d['ms_per_step'],4))"
+  done
+}
+
 case "$1" in
   series) task_series ;;
   learner-prof) task_learner_prof ;;
@@ -178,5 +188,6 @@ case "$1" in
   full) task_full ;;
   final-bench) task_final_bench ;;
   shape-sweep) task_shape_sweep ;;
-  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep}"; exit 2 ;;
+  configs) task_configs ;;
+  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep|configs}"; exit 2 ;;
 esac

@@ -901,7 +901,6 @@ class FFMPVec:
             raise RuntimeError("call reset() before temporal_maps()")
         N, G = self.num_envs, self.cfg.grid
         if self.frame_window == 2:
-            lag_slots = None
             offs = [G * G, 0]  # contiguous (N, 2, G, G): newest, older
             env_stride = 2 * G * G
         else:
@@ -910,8 +909,7 @@ class FFMPVec:
                                    f"temporal_maps({k}) needs {k} (step {k - len(self._hist)} more times, or reset())")
             # lags the ring has not seen since a full reset are never read (every env's lag is
             # clamped to its steps since that reset): any valid slot stands in
-            lag_slots = [self._hist[min(d, len(self._hist) - 1)] for d in range(k)]
-            offs = [s * self.frames.stride(0) for s in lag_slots]
+            offs = [self._hist[min(d, len(self._hist) - 1)] * self.frames.stride(0) for d in range(k)]
             env_stride = G * G
         offs = (offs + [offs[-1]] * k)[:k]
         if out is None:

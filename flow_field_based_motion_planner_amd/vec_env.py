@@ -141,10 +141,8 @@ class FFMPVec:
         self._alloc()
         G2 = self.cfg.grid * self.cfg.grid
         if pipeline is None:
-            pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt)
+            pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt, r03b_pipeline.txt)
         self.pipeline_slices = max(1, min(int(pipeline), self.num_envs))
-        if self.pipeline_slices > 1 and self.frame_window != 2:
-            raise ValueError("pipeline > 1 needs frame_window=2")
         if self.pipeline_slices > 1 and fused:
             raise ValueError("pipeline > 1 and fused=True are exclusive")
         if self.pipeline_slices > 1:
@@ -489,8 +487,9 @@ class FFMPVec:
             self.step(a, timing=t)
         torch.cuda.synchronize(self.device)
         per: Dict[int, list] = {}
-        for k, r in enumerate(t):
-            per.setdefault(self._slot_written(k), []).append(r[0].elapsed_time(r[1]))
+        S = self.pipeline_slices  # timing entries per step (one raster launch per env slice)
+        for k in range(len(t) // S):
+            per.setdefault(self._slot_written(k), []).append(sum(r[0].elapsed_time(r[1]) for r in t[k * S:(k + 1) * S]))
         self._clear_after_tuning()
         return {i: float(np.median(v)) for i, v in per.items()}
 
@@ -830,6 +829,7 @@ class FFMPVec:
             lo, hi = torch.cuda.Stream.priority_range()
             self._side = torch.cuda.Stream(self.device, priority=hi)  # env kernels first
             self._ev_go = torch.cuda.Event()
+        if S > 1 and len(getattr(self, "_ev_slice", ())) != S:
             self._ev_slice = [torch.cuda.Event() for _ in range(S)]
 
     def _stream(self):
@@ -1067,17 +1067,25 @@ class FFMPVec:
                                                 a.data_ptr() + a0 * 8, C.byref(st), C.byref(ob), C.byref(out), sp),
                        "ffmp_step_state")
             self._ev_slice[k].record(side)
+        # the raster of slice k on the main stream once its env slice is done: the env kernels of the
+        # later slices run beside it.  The frame pair slides as in raster_step (ring or contiguous).
+        full = self._next_window()
+        cpb, flags = self.raster_shape if full else self.raster_shape_newest
+        flags |= 0 if full else _abi.RASTER_NEWEST
+        sm0, sm_stride, sm_frame = self._obs_c.state_m, self._obs_c.state_m_stride, self._obs_c.state_m_frame_stride
         mp = C.c_void_p(main.cuda_stream)
         for k, (a0, n, st, ob, out, rec) in enumerate(self._slices):
+            ob.state_m = sm0 + a0 * sm_stride * self._fes
+            ob.state_m_stride, ob.state_m_frame_stride = sm_stride, sm_frame
             main.wait_event(self._ev_slice[k])
             if timing is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(main)
-            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), n, rec, None, C.byref(ob), *self.raster_shape, mp),
+            _abi.check(self.lib.ffmp_raster_ex(C.byref(self._cfg_c), n, rec, None, C.byref(ob), cpb, flags, mp),
                        "ffmp_raster")
             if timing is not None:
                 e1.record(main)
-                timing.append((e0, e1, n, self._raster_bytes(n, True), True))
+                timing.append((e0, e1, n, self._raster_bytes(n, full), full))
 
     def step(self, actions, copy: bool = False, timing: Optional[list] = None
              ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor, dict]:

@@ -233,23 +233,26 @@ def test_exactness_report(capsys):
     assert rep["record"] == 0
 
 
-@pytest.mark.parametrize("slices", [2, 5])
-def test_pipelined_step_equals_serial(slices):
+@pytest.mark.parametrize("slices,window", [(2, None), (5, None), (3, 4), (2, 8)])
+def test_pipelined_step_equals_serial(slices, window):
     """The two-stream pipelined step (env kernel of slice s+1 beside the raster of slice s)
-    produces exactly the serial step's tensors."""
+    produces exactly the serial step's tensors — contiguous frames or the seamless ring (newest-only
+    rasters per slice, the pair sliding through every slot incl. the alias)."""
     cfg = FFMPConfig(grid=64, n_obst=12, n_beams=32, moving=True, obst_rmax=0.5, seed=41)
-    ser = FFMPVec(83, cfg, device="cuda:0", pipeline=1)
-    pip = FFMPVec(83, cfg, device="cuda:0", pipeline=slices)
+    ser = FFMPVec(83, cfg, device="cuda:0", pipeline=1, frame_window=window)
+    pip = FFMPVec(83, cfg, device="cuda:0", pipeline=slices, frame_window=window)
+    assert pip.ring == ser.ring and (window is None or pip.ring == "seamless")
     assert pip.pipeline_slices == slices and ser.pipeline_slices == 1
     ser.reset()
     pip.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(5)
-    for _ in range(8):
+    for _ in range(19):
         a = torch.randint(0, 28, (83,), device="cuda:0", generator=gen)
         t1, t2 = [], []
         ser.step(a, timing=t1)
         pip.step(a, timing=t2)
         assert len(t1) == 1 and len(t2) == slices and sum(r[2] for r in t2) == 83
+        assert torch.equal(ser.state_m, pip.state_m)
     torch.cuda.synchronize()
     g1, g2 = gpu_snapshot(ser), gpu_snapshot(pip)
     for k in g1:

@@ -18,6 +18,7 @@
 #   full              round 3 (second session): the whole GPU suite as the driver runs it, then smoke()
 #   shape-sweep       steady-state raster time of launch shapes beyond the autotune's (tools/shape_sweep.py)
 #   configs           the other BASELINE configs' bench lines (C2, the C5 per-GPU share)
+#   pipeline          the two-launch step with its env kernel in slices beside the raster (tools/pipeline_probe.py)
 #   final-bench       round 3 (second session): the driver's bench command line on the final code, two fresh processes
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -170,6 +171,10 @@ print('$c', round(d['value']/1e6,3), 'M', r['kernel'], round(r['kernel_ms'],4), 
   done
 }
 
+task_pipeline() {
+  timeout -k 10 300 python3 tools/pipeline_probe.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r03b_pipeline.txt
+}
+
 case "$1" in
   series) task_series ;;
   learner-prof) task_learner_prof ;;
@@ -189,5 +194,6 @@ case "$1" in
   final-bench) task_final_bench ;;
   shape-sweep) task_shape_sweep ;;
   configs) task_configs ;;
-  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep|configs}"; exit 2 ;;
+  pipeline) task_pipeline ;;
+  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep|configs|pipeline}"; exit 2 ;;
 esac

@@ -19,6 +19,7 @@
 #   shape-sweep       steady-state raster time of launch shapes beyond the autotune's (tools/shape_sweep.py)
 #   configs           the other BASELINE configs' bench lines (C2, the C5 per-GPU share)
 #   pipeline          the two-launch step with its env kernel in slices beside the raster (tools/pipeline_probe.py)
+#   two-rank          bench.py --gpus 2 over gloo with both ranks on the one GPU (the N > 1 code path)
 #   final-bench       round 3 (second session): the driver's bench command line on the final code, two fresh processes
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -175,6 +176,13 @@ task_pipeline() {
   timeout -k 10 300 python3 tools/pipeline_probe.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r03b_pipeline.txt
 }
 
+task_two_rank() {
+  timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --cpu-seconds 0 > gpurun_out/r03b_two_rank.log 2>&1 || { tail -30 gpurun_out/r03b_two_rank.log; exit 1; }
+  grep '^{' gpurun_out/r03b_two_rank.log | tail -1 | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); s=d.get('strong') or {}
+print('n_gpus', d['n_gpus'], 'world_size_backend', d['config']['world_size_backend'], 'weak', round(d['value']/1e6,3), 'per-rank ms', d['per_rank_ms_per_step'], '| strong', round(s.get('value',0)/1e6,3), s.get('per_rank_ms_per_step'), '| compact', d.get('compact_layout'))"
+}
+
 case "$1" in
   series) task_series ;;
   learner-prof) task_learner_prof ;;
@@ -195,5 +203,6 @@ case "$1" in
   shape-sweep) task_shape_sweep ;;
   configs) task_configs ;;
   pipeline) task_pipeline ;;
-  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep|configs|pipeline}"; exit 2 ;;
+  two-rank) task_two_rank ;;
+  *) echo "usage: $0 {series|learner-prof|spec|conv|learner|ct8|ct8-check|compact-fresh|bench|launches|benchloop|transient|transient-shapes|transient-reset|full|final-bench|shape-sweep|configs|pipeline|two-rank}"; exit 2 ;;
 esac

@@ -294,7 +294,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     from flow_field_based_motion_planner_amd.vec_env import FFMPVec
     fb = 4 if args.obs_format == "f32" else 1
     # the actions first: the first use of torch's random kernels loads their code (a GPU-idle gap),
-    # and after an idle gap the raster runs slow for ~10 steps while the clocks ramp back up
+    # and after such a gap the raster runs slow for about one ring cycle while the GPU warms up again
     # (profiles/r03b_transient*.txt) — here that gap falls before construction, not before the warm-up
     gen = torch.Generator(device=dev).manual_seed(1000 + rank + (0 if main_leg else 5000))
     actions = torch.randint(0, 28, (W + K, n), device=dev, dtype=torch.int64, generator=gen)
@@ -312,8 +312,8 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
             json.dump(env.tuning(), f)
     free, total = torch.cuda.mem_get_info(dev)
     # the torch kernel the loop's bookkeeping uses (episode.sum) is loaded now: its first call loads
-    # its code with the GPU idle, and after such a gap the raster runs slow for ~10 steps while the
-    # clocks ramp back up (profiles/r03b_transient_loop.txt) — it must not fall between the warm-up
+    # its code with the GPU idle, and after such a gap the raster runs slow for about one ring cycle
+    # (profiles/r03b_transient_loop.txt) — it must not fall between the warm-up
     # and the timed steps
     int(env.episode.sum())
     env.reset()

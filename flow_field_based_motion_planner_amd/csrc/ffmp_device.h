@@ -364,6 +364,66 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x
   return best;
 }
 
+// CH beams of one lane at a time (beams l0, l0 + lpe, ..., l0 + (CH-1) lpe): the disc loop is
+// outermost, so each disc's four LDS operands are read once per CH beams and the CH beams' tests
+// are independent chains.  Every beam sees exactly lidar_beam's operations in lidar_beam's order
+// (discs in ascending k, then the walls), so every range is bit-identical to it.
+// f(l, range) for every beam l < n_beams of this lane.
+template <int CH, class F>
+FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane, int lpe, double x, double y,
+                          double c, double s, const double* rxa, const double* rya, const double* rra,
+                          const double* r2a, F&& f) {
+  const double inf = __builtin_inf();
+  const double2* bt = reinterpret_cast<const double2*>(cfg.beam_cs);
+  const int nb = cfg.n_beams;
+  const double W = cfg.world_half, L = cfg.lidar_max;
+  for (int l0 = lane; l0 < nb; l0 += CH * lpe) {
+    double dirx[CH], diry[CH], best[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int l = l0 + j * lpe;
+      const double2 b = l < nb ? bt[l] : make_double2(1.0, 0.0);
+      dirx[j] = c * b.x - s * b.y;
+      diry[j] = s * b.x + c * b.y;
+      best[j] = inf;
+    }
+    if (!sc.inside) {
+      for (uint64_t m = sc.mask; m; m &= m - 1) {
+        const int k = __builtin_ctzll(m);
+        const double rx = rxa[k], ry = rya[k];
+        const double rr = rra[k];
+        const double r2 = r2a[k];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const double tp = rx * dirx[j] + ry * diry[j];
+          if (tp > 0.0) {
+            const double perp = rr - tp * tp;
+            if (perp <= r2) {
+              const double h = tp - sqrt(r2 - perp);
+              if (h <= L && h < best[j]) best[j] = h;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const double dx = dirx[j], dy = diry[j];
+        double bj = best[j];
+        if (dx > 0.0) { if (sc.wxp && wall_in_reach(W - x, dx, L)) { const double h = (W - x) / dx; if (h <= L && h < bj) bj = h; } }
+        else if (dx < 0.0) { if (sc.wxn && wall_in_reach(-W - x, dx, L)) { const double h = (-W - x) / dx; if (h <= L && h < bj) bj = h; } }
+        if (dy > 0.0) { if (sc.wyp && wall_in_reach(W - y, dy, L)) { const double h = (W - y) / dy; if (h <= L && h < bj) bj = h; } }
+        else if (dy < 0.0) { if (sc.wyn && wall_in_reach(-W - y, dy, L)) { const double h = (-W - y) / dy; if (h <= L && h < bj) bj = h; } }
+        best[j] = bj;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int l = l0 + j * lpe;
+      if (l < nb) f(l, sc.inside ? -inf : best[j]);
+    }
+  }
+}
+
 // FFMP.is_collision2 on one float32 beam (ffmp.py:110-115): `if r:` skips 0,
 // `r < ROBOT_RSIZE` is a float64 compare.
 FFMP_DEV bool beam_collides(float r, double thr) { return (r != 0.0f) && ((double)r < thr); }

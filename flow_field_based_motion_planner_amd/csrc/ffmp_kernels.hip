@@ -193,6 +193,14 @@ FFMP_DEV double2 first_beam(const ffmp_cfg_t& cfg, int lane) {
   return lane < cfg.n_beams ? reinterpret_cast<const double2*>(cfg.beam_cs)[lane] : make_double2(0.0, 0.0);
 }
 
+// Beams traced per lane at a time (trace_beams in ffmp_device.h); 1 = one beam at a time,
+// lidar_beam with the table read one beam ahead.  3: C3's env kernel 87.4-88.3 -> 78.5-79.4 us, C5
+// share 92.1 -> 82.8 (2 -> 80.7-81.3 / 85.2; 4 -> 92 at 131 VGPRs, 3 waves per SIMD;
+// profiles/r03c_beam_chunk.txt), bit-identical ranges.
+#ifndef FFMP_BEAM_CHUNK
+#define FFMP_BEAM_CHUNK 3
+#endif
+
 template <class F>
 FFMP_DEV void for_beams(const ffmp_cfg_t& cfg, int lane, int lpe, double2 b, F&& f) {
   const double2* bt = reinterpret_cast<const double2*>(cfg.beam_cs);
@@ -220,7 +228,7 @@ FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, int2* s_foot) {
 // cells are strided over the group's lanes.
 // One env's step (or reset) by its LPE-lane group: lane = the lane within the group, s_* = the
 // group's LDS slices (FFMP_MAX_OBST entries each).  Used by env_kernel and step_raster_kernel.
-template <int MODE, int LPE>
+template <int MODE, int LPE, int BCH = FFMP_BEAM_CHUNK>
 FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, int64_t env_offset,
                                                        const int64_t* __restrict__ action, int32_t initial,
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
@@ -317,11 +325,19 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
-      const float rf = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
-      ob.lidar[e * L + l] = rf;
-      c_lidar |= beam_collides(rf, cfg.robot_r);
-    });
+    if constexpr (BCH > 1) {
+      trace_beams<BCH>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, [&](int l, double r) {
+        const float rf = (float)r;
+        ob.lidar[e * L + l] = rf;
+        c_lidar |= beam_collides(rf, cfg.robot_r);
+      });
+    } else {
+      for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
+        const float rf = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
+        ob.lidar[e * L + l] = rf;
+        c_lidar |= beam_collides(rf, cfg.robot_r);
+      });
+    }
     FFMP_ENV_STAMP(8);
     c_foot = group_ballot(c_foot, LPE) != 0;
     c_lidar = (group_ballot(c_lidar, LPE) != 0) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
@@ -379,9 +395,14 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
-      ob.lidar[e * L + l] = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
-    });
+    if constexpr (BCH > 1) {
+      trace_beams<BCH>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or,
+                                   [&](int l, double r) { ob.lidar[e * L + l] = (float)r; });
+    } else {
+      for_beams(cfg, lane, LPE, beam0, [&](int l, double2 b) {
+        ob.lidar[e * L + l] = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
+      });
+    }
   }
 
   FFMP_ENV_STAMP(4);
@@ -1032,7 +1053,9 @@ __global__ __launch_bounds__(256, (kFusedMinWaves<FLOW, FMT>)) void step_raster_
   FFMP_RAS_STAMP(0);
   if (threadIdx.x < 64) {
     stage_footprint(cfg, s_foot);
-    env_group<kEnvMode_Step, 64>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
+    // (one beam at a time where the block is held to more than 4 waves per SIMD: the chunked
+    // lidar's registers would spill there)
+    env_group<kEnvMode_Step, 64, (kFusedMinWaves<FLOW, FMT> > 4 ? 1 : FFMP_BEAM_CHUNK)>(cfg, env_offset, action, 0, st, ob, out, e, (int)threadIdx.x, s_ox, s_oy, s_or,
                                  s_orr, s_ecur, s_eprev, s_foot, s_hdr, FLOW ? s_vel : nullptr);
   }
   // The record reaches the raster through LDS: env_group left its ego discs of both frames in

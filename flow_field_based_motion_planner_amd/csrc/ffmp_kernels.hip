@@ -1479,11 +1479,13 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
   if (n > 0x7fffffffLL / 64) return fail(FFMP_E_ARG, "n too large for one launch: %lld", (long long)n);  // <= 64 lanes per env
   ffmp_out_t o = out ? *out : ffmp_out_t{};
   const Tuning& tu = tuning();
-  // lanes per env: at least K (lane k holds disc k); with many beams more lanes keep the lidar
-  // loop short (profiles/r01_env_kernel.txt: C3 with L = 180 is fastest at 32, L = 64 at 16)
+  // lanes per env: the fewest that hold the discs (lane k holds disc k).  Round 1 gave many-beam
+  // configs more lanes to keep the one-beam-at-a-time lidar loop short; with three beams per chunk
+  // the per-env scalar work dominates and fewer, longer beam loops win: C3 (K = 16, L = 180) 79 us
+  // at 32 lanes -> 68 at 16, the C5 share (K = 32, L = 360) 83 at 64 -> 77 at 32
+  // (profiles/r03c_beam_chunk.txt).
   const int need = cfg->n_obst <= 16 ? 16 : cfg->n_obst <= 32 ? 32 : 64;
-  const int want_l = cfg->n_beams <= 128 ? 16 : cfg->n_beams <= 256 ? 32 : 64;
-  const int autol = need > want_l ? need : want_l;
+  const int autol = need;
   const int lpe = tu.env_lanes ? (tu.env_lanes >= need ? tu.env_lanes : need) : autol;
   if (tu.env_waves == 4)
     launch_env_lpe<4>(mode, lpe, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, (hipStream_t)stream);

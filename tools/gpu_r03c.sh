@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 3, last session: GPU tasks.  usage: bash tools/gpu_r03c.sh <task>
 #   full-bench   the whole -m gpu suite + smoke(), then the driver's bench command twice
+#   prof         rocprofv3 kernel trace + stats of the bench (C3 legs, no CPU leg)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
@@ -20,8 +21,19 @@ print('f32', round(d['value']/1e6,3), 'step', round(d['ms_per_step'],4), r['kern
   done
 }
 
+task_prof() {
+  rm -rf gpurun_out/prof_r03c
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r03c -o c3 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/r03c_prof_bench.log 2>&1 || { tail -20 gpurun_out/r03c_prof_bench.log; exit 1; }
+  f=$(find gpurun_out/prof_r03c -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/r03c_C3_final_kernel_stats.csv
+  python3 -c "
+import csv; rows=list(csv.DictReader(open('gpurun_out/r03c_C3_final_kernel_stats.csv')))
+for r in rows[:8]: print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')"
+  tail -1 gpurun_out/r03c_prof_bench.log | cut -c1-300
+}
+
 case "$1" in
+  prof) task_prof ;;
   full-bench) task_full && task_bench ;;
   bench) task_bench ;;
-  *) echo "usage: $0 {full-bench|bench}"; exit 2 ;;
+  *) echo "usage: $0 {full-bench|bench|prof}"; exit 2 ;;
 esac

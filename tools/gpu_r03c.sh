@@ -23,7 +23,7 @@ print('f32', round(d['value']/1e6,3), 'step', round(d['ms_per_step'],4), r['kern
 
 task_prof() {
   rm -rf gpurun_out/prof_r03c
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r03c -o c3 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/r03c_prof_bench.log 2>&1 || { tail -20 gpurun_out/r03c_prof_bench.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r03c -o c3 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/r03c_prof_bench.log 2>&1 || { tail -20 gpurun_out/r03c_prof_bench.log; exit 1; }
   f=$(find gpurun_out/prof_r03c -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/r03c_C3_final_kernel_stats.csv
   python3 -c "
 import csv; rows=list(csv.DictReader(open('gpurun_out/r03c_C3_final_kernel_stats.csv')))

@@ -1,5 +1,7 @@
 #!/bin/bash
 # lidar beams traced CH at a time per lane (trace_beams, FFMP_BEAM_CHUNK): whole-config oracle
+# builds first, on the CPU: for ch in 1 2 3 4 6: hipcc (the Makefile's HIPFLAGS) -DFFMP_BEAM_CHUNK=$ch
+#   -o tools/_build/libffmp_ch$ch.so <the three csrc/*.hip>
 # parity with each chunked build, then the env kernel alone, alternating builds (C3, C5, C2)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}

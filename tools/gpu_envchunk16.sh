@@ -1,5 +1,7 @@
 #!/bin/bash
 # env kernel at the fewest lanes per env (the new auto rule) by beams per chunk (ch3 = default build)
+# builds first, on the CPU: for ch in 1 2 3 4 6: hipcc (the Makefile's HIPFLAGS) -DFFMP_BEAM_CHUNK=$ch
+#   -o tools/_build/libffmp_ch$ch.so <the three csrc/*.hip>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 B=$R/tools/_build

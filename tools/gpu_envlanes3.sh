@@ -1,5 +1,7 @@
 #!/bin/bash
 # env kernel by lanes per env and waves per block with the chunked lidar (ch3 = default build, ch2)
+# builds first, on the CPU: for ch in 1 2 3 4 6: hipcc (the Makefile's HIPFLAGS) -DFFMP_BEAM_CHUNK=$ch
+#   -o tools/_build/libffmp_ch$ch.so <the three csrc/*.hip>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 B=$R/tools/_build

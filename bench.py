@@ -11,6 +11,11 @@ in HBM before the timed region).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset), this process starts the N rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in each
+child's environment) before anything touches the GPU, waits for them and exits with the first
+non-zero status; every rank checks that its process group has exactly N members.
+
 N=1 workload: BASELINE config C3 (32,768 envs, 256x256 grid, 16 moving discs,
 180-beam lidar) — the largest single-GPU config and the one the north-star
 target (256x256, 32k envs) is quoted on.  Every run has two legs:
@@ -268,7 +273,12 @@ def time_compact_child(name, steps, seed):
             "frame_window": d["config"]["frame_window"], "ring": d["config"]["ring"], "fused": d["config"]["fused"],
             "shape": a.get("shape_newest"), "construct_s": d.get("construct_s"), "hbm_bytes": d.get("hbm_bytes"),
             "ring_pairing": {k: ring.get(k) for k in ("pieces", "pair_probes", "pair_gbs_min", "pair_gbs_max",
-                                                      "partner_tries", "rebuilds", "reverts")},
+                                                      "partner_tries", "rebuilds", "reverts", "repair",
+                                                      "pool_released_bytes")},
+            # the child's launch decisions, for audit: every raster-shape candidate's GB/s, the
+            # one-launch vs two-launch step times (autotune and post-repair recheck), the flags kept
+            "autotune": {k: a.get(k) for k in ("shape", "shape_newest", "gbs", "candidates", "fused")},
+            "hbm_in_use_bytes": d.get("hbm_in_use_bytes"),
             "process": "a child process of its own (bench.py --obs-format u8f16)"}
 
 
@@ -363,6 +373,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         "per_rank_construct_s": [round(r[1], 2) for r in per_rank],
         "construct_s": round(construct_s, 2), "hbm_bytes": env.hbm_bytes(),
         "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
+        "pool_released_bytes": getattr(env, "pool_released_bytes", 0),
         "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
@@ -408,8 +419,56 @@ def _leg_size(name, args, world, dev):
     return cfg, n, strong
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd=None) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank children of this same command line, one
+    per GPU, with the torchrun environment variables set, and wait for all of them.  Called before
+    torch is imported, so this parent never initialises the GPU (no HIP call, no exec)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FFMP_BENCH_LAUNCHER="1")
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:  # one rank failed: the others would wait in a collective forever
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        rc = 130
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
     from flow_field_based_motion_planner_amd.vec_env import FFMPVec
@@ -417,8 +476,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: WORLD_SIZE={world} but --gpus={args.gpus} (run with torchrun --nproc-per-node {args.gpus}, "
+              f"or without WORLD_SIZE set and bench.py starts the ranks)", file=sys.stderr)
+        sys.exit(2)
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
@@ -428,6 +489,9 @@ def main():
         else:
             dist.init_process_group("gloo")
     pg_world = dist.get_world_size() if world > 1 else 1  # as the collective backend sees it
+    if pg_world != args.gpus:
+        print(f"error: the process group has {pg_world} ranks, --gpus={args.gpus}", file=sys.stderr)
+        sys.exit(2)
 
     name = args.config
     cfg, n, strong = _leg_size(name, args, world, dev)
@@ -484,13 +548,19 @@ def main():
                        "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
                        "frame_window": leg["frame_window"], "ring": leg["ring"], "fused": leg["fused"],
                        "parallelism": f"env-shard x{world}",
-                       "comm": (args.dist_backend if world > 1 else "none"), "world_size_backend": pg_world},
+                       "comm": (args.dist_backend if world > 1 else "none"), "world_size_backend": pg_world,
+                       "launcher": ("bench.py" if os.environ.get("FFMP_BENCH_LAUNCHER") else
+                                    "torchrun" if "WORLD_SIZE" in os.environ else "none")},
             "roofline": rl,
             "per_rank_ms_per_step": leg["per_rank_ms_per_step"],
             "construct_s": leg["construct_s"],
             "per_rank_construct_s": leg["per_rank_construct_s"],
             "hbm_bytes": leg["hbm_bytes"],
             "hbm_in_use_bytes": leg["hbm_in_use_bytes"],
+            # HBM the process holds beyond the instance (torch context, caches); round 3 parked ~65 GB
+            # of unchosen ring pieces here, now released after construction (pool_released_bytes)
+            "hbm_beyond_instance_bytes": leg["hbm_in_use_bytes"] - leg["hbm_bytes"],
+            "pool_released_bytes": leg["pool_released_bytes"],
             "raster_ms_per_step": leg["raster_ms_per_step"],
             "step_ms_events": leg["step_ms_events"],
             "pipeline_slices": leg["pipeline_slices"],

@@ -58,7 +58,9 @@ def main():
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed,
                      flow=args.input_channels == 3 and not args.temporal_maps)
-    window = max(args.input_channels, 3) if args.temporal_maps else None
+    # k + 1 slots: enough on a wrapping ring too (the fallback on devices without HIP VMM), which
+    # holds W - 1 distinct frames once it has wrapped (FFMPVec.max_temporal_frames)
+    window = max(args.input_channels + 1, 3) if args.temporal_maps else None
     env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format, frame_window=window)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
                   mfma=False if args.no_mfma else None,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 OBS_F32, OBS_U8F16 = 0, 1  # include/ffmp.h FFMP_OBS_*
 MAX_SERIES = 16  # FFMP_MAX_SERIES (ffmp_temporal_maps)
 
@@ -116,6 +116,7 @@ _SIGS = {
     "ffmp_conv2d_fwd_bf16": (C.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32,
                                        _P]),
     "ffmp_conv2d_wgrad_bf16": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    "ffmp_conv2d_check": (C.c_int, [_I32] * 10),
     "ffmp_episode_init": (C.c_int, [_I64, _P, _I32, C.POINTER(EpisodeT), _P]),
     "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
                                       _P]),
@@ -125,6 +126,7 @@ _SIGS = {
     "ffmp_ring_rebuild": (C.c_int, [_P, C.c_uint64, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "ffmp_ring_destroy": (C.c_int, [_P]),
     "ffmp_ring_pool_bytes": (_I64, [_I32]),
+    "ffmp_ring_pool_trim": (C.c_int, [_I32, _I64, C.POINTER(_I64)]),
     "ffmp_dlpack": (_P, [_P, _I32, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64), _I32, _P]),
 }
 
@@ -213,6 +215,15 @@ def set_tuning(key: int, value: int) -> int:
     if prev < 0:
         check(prev, "ffmp_set_tuning")
     return prev
+
+
+def ring_pool_trim(device: int, keep_bytes: int = 0) -> int:
+    """Give back the physical memory of the frame-ring pieces parked in the process pool of
+    `device` beyond keep_bytes (include/ffmp.h ffmp_ring_pool_trim; the addresses stay reserved).
+    Returns the bytes released."""
+    out = C.c_int64(0)
+    check(load().ffmp_ring_pool_trim(int(device), int(keep_bytes), C.byref(out)), "ffmp_ring_pool_trim")
+    return int(out.value)
 
 
 # ----------------------------------------------------------------- DLPack (device memory -> torch)

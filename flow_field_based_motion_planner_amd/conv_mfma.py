@@ -19,6 +19,7 @@ loop: no per-shape kernel search on a fresh box.
 from __future__ import annotations
 
 import ctypes as C
+import functools
 from typing import Optional
 
 import torch
@@ -28,10 +29,36 @@ from . import _abi
 CONV_RELU, CONV_OUT_BF16 = 1, 2  # include/ffmp.h FFMP_CONV_*
 
 
-def supported(conv: torch.nn.Conv2d) -> bool:
-    """Stride 1, no padding / dilation / groups, 32 or 64 channels in and out (the kernel's shapes)."""
+def _layer_ok(conv: torch.nn.Conv2d) -> bool:
     return (conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1
-            and conv.in_channels in (32, 64) and conv.out_channels in (32, 64) and conv.padding_mode == "zeros")
+            and conv.padding_mode == "zeros")
+
+
+@functools.lru_cache(maxsize=1024)
+def shape_ok(kind: int, batch: int, h: int, w: int, c: int, kh: int, kw: int, n: int, pad: int = 0, dx: int = 1) -> bool:
+    """Does the kernel take this shape (include/ffmp.h ffmp_conv2d_check: the launch's own checks,
+    nothing launched)?  kind 0: forward / data gradient (pad > 0), 1: weight gradient."""
+    return _abi.load().ffmp_conv2d_check(kind, batch, h, w, c, kh, kw, n, pad, dx) == 0
+
+
+def supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
+    """Stride 1, no padding / dilation / groups, 32 or 64 channels in and out (the kernel's layers);
+    with the input's NCHW shape, also every launch the layer's forward and backward make: the
+    forward, the data gradient (the padded full convolution of the output gradient) and the weight
+    gradient — input rows of <= 16 KiB, batch <= 65535, the LDS ring, weight-gradient rows of >= 8
+    positions.  False: the caller keeps the library convolution for this shape."""
+    if not (_layer_ok(conv) and conv.in_channels in (32, 64) and conv.out_channels in (32, 64)):
+        return False
+    if x_shape is None:
+        return True
+    B, C, H, W = (int(v) for v in x_shape)
+    KH, KW = conv.kernel_size
+    N = conv.out_channels
+    Ho, Wo = H - KH + 1, W - KW + 1
+    if C != conv.in_channels or Ho < 1 or Wo < 1:
+        return False
+    return (shape_ok(0, B, H, W, C, KH, KW, N) and shape_ok(0, B, Ho, Wo, N, KH, KW, C, KH - 1)
+            and shape_ok(1, B, H, W, C, KH, KW, N))
 
 
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
@@ -96,7 +123,8 @@ def conv2d_wgrad_nhwc(g: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dx: in
 
 class MFMAConv2dReLU(torch.autograd.Function):
     """relu(conv2d(x, weight, bias)) in bf16 with fp32 accumulation; returns a bf16 NCHW-shaped
-    tensor (channels-last strides)."""
+    tensor (channels-last strides).  The bias is added in fp32 (autocast's conv2d rounds it to
+    bf16 first: a difference of at most half a bf16 ulp of the bias)."""
 
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
@@ -138,11 +166,22 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 #   y[b, yo, xo, n] = sum_{ky, kx', q} x'[b, yo+ky, xo+kx'*F, q] w'[ky, kx', n, q]
 # the same products and sum as the original, on the MFMA kernel.
 
-def fold_supported(conv: torch.nn.Conv2d) -> bool:
+def fold_supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
+    """A 1-4 channel layer whose kernel width folds into 32 channels; with the input's NCHW shape,
+    also the folded forward and weight-gradient launches (the input gradient is MIOpen's)."""
     c = conv.in_channels
-    return (conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1
-            and c in (1, 2, 3, 4) and conv.kernel_size[1] % (32 // (4 if c == 3 else c)) == 0
-            and conv.out_channels in (32, 64))
+    if not (_layer_ok(conv) and c in (1, 2, 3, 4) and conv.kernel_size[1] % (32 // (4 if c == 3 else c)) == 0
+            and conv.out_channels in (32, 64)):
+        return False
+    if x_shape is None:
+        return True
+    B, Cx, H, W = (int(v) for v in x_shape)
+    KH, KW = conv.kernel_size
+    F = 32 // (4 if c == 3 else c)
+    if Cx != c or H < KH or W < KW:
+        return False
+    return (shape_ok(0, B, H, W - F + 1, 32, KH, KW // F, conv.out_channels, 0, F)
+            and shape_ok(1, B, H, W - F + 1, 32, KH, KW // F, conv.out_channels, 0, F))
 
 
 def fold_input(x: torch.Tensor, F: int) -> torch.Tensor:

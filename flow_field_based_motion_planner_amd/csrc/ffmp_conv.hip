@@ -32,8 +32,11 @@
 
 namespace ffmp_detail {
 int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_error())
+// ffmp_conv2d_check: run every shape check of a launch, then return before launching
+thread_local bool t_conv_dry = false;
 }
 using ffmp_detail::fail;
+using ffmp_detail::t_conv_dry;
 
 namespace {
 
@@ -362,6 +365,7 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
   const dim3 grid((Ho * Wo + 127) / 128, B);
+  if (t_conv_dry) return FFMP_OK;
   hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w,
                      bias, y, H, W, KH, KW, pad, dx, flags);
   const hipError_t e = hipGetLastError();
@@ -406,6 +410,7 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
     return fail(FFMP_E_ARG, "ffmp_conv2d: a ring of %d input rows (%zu bytes) exceeds the 160 KiB LDS", ring, lds);
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
+  if (t_conv_dry) return FFMP_OK;
   hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
                      y, H, W, KH, KW, pad, dx, ring, flags);
   const hipError_t e = hipGetLastError();
@@ -645,6 +650,7 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   if (Wo < 8) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: output rows of %d < 8 positions", Wo);
   const int per_chunk = (B + chunks - 1) / chunks;
   const dim3 grid((KH / TKY) * (KW / TKX), (B + per_chunk - 1) / per_chunk);
+  if (t_conv_dry) return FFMP_OK;
   hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW>), grid, dim3(256), bytes(R), s, (const __bf16*)g, (const __bf16*)x,
                      part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
   const hipError_t e = hipGetLastError();
@@ -692,6 +698,18 @@ int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t ba
   if (c == 32 && n == 32) return launch_wgrad<32, 32, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 64 && n == 32) return launch_wgrad<64, 32, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: channels in/out must be 32 or 64 (got %d / %d)", c, n);
+}
+
+int ffmp_conv2d_check(int32_t kind, int32_t batch, int32_t h, int32_t wd, int32_t c, int32_t kh, int32_t kw,
+                      int32_t n, int32_t pad, int32_t dx) {
+  // aligned stand-in pointers: nothing is read or launched in a dry run
+  void* const p = reinterpret_cast<void*>(static_cast<uintptr_t>(256));
+  t_conv_dry = true;
+  const int rc = kind == 0 ? ffmp_conv2d_fwd_bf16(p, p, nullptr, p, batch, h, wd, c, kh, kw, n, pad, dx, 0, nullptr)
+               : kind == 1 ? ffmp_conv2d_wgrad_bf16(p, p, static_cast<float*>(p), batch, h, wd, c, kh, kw, n, dx, 1, nullptr)
+                           : fail(FFMP_E_ARG, "ffmp_conv2d_check: kind must be 0 (forward / data gradient) or 1 (weight gradient)");
+  t_conv_dry = false;
+  return rc;
 }
 
 }  // extern "C"

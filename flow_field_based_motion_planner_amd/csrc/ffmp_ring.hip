@@ -41,13 +41,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //   candidates from the free-piece
 //   pool first, then fresh pieces; pieces that pair badly here stay pooled for other positions
 //   or later rings.
-// * Never unmap.  Once a VMM range is unmapped and its address reused by a new mapping, the
-//   runtime can still resolve the address to the OLD allocation (tools/ring_reuse_probe.hip:
-//   D2H copies of a fresh mapping return the previous ring's bytes; FFMPVec saw the first
-//   raster into a fresh ring vanish).  So nothing is ever unmapped before exit: every piece
-//   keeps a private "home" mapping, a ring maps its pieces once more at a fresh address, and a
-//   ring whose last reference is dropped returns its pieces to the pool (its addresses are
-//   simply never used again).
+// * Never reuse an address.  Once a VMM range is unmapped and its address reused by a new
+//   mapping, the runtime can still resolve the address to the OLD allocation
+//   (tools/ring_reuse_probe.hip: D2H copies of a fresh mapping return the previous ring's bytes;
+//   FFMPVec saw the first raster into a fresh ring vanish).  So no reservation is ever freed:
+//   every piece keeps a private "home" mapping, a ring maps its pieces once more at a fresh
+//   address, and a ring whose last reference is dropped returns its pieces to the pool (its
+//   addresses are simply never used again).  A pooled piece's physical memory can still be given
+//   back (ffmp_ring_pool_trim): every mapping of it (home and the dead rings') is unmapped and the
+//   handle released, while the address ranges stay reserved — no later mapping can land there.
 // * Sharing.  A piece may sit in several rings at once: ffmp_ring_rebuild leaves `old` whole
 //   and maps its kept pieces into the new ring too, so that a caller can time both and keep
 //   the faster.  Each piece carries a count of the rings holding it; it is retired when the
@@ -61,6 +63,7 @@ struct ffmp_piece {
   size_t bytes;
   int32_t device;
   int* rings;  // rings holding the piece (shared by every copy; under g_pool_mu)
+  std::vector<char*>* maps;  // every address it is mapped at: home, then each ring's (shared; under g_pool_mu)
 };
 
 struct ffmp_ring {
@@ -186,7 +189,6 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
   p.device = device;
   hipError_t e = hipMemCreate(&p.h, bytes, &prop, 0);
   if (e != hipSuccess) return e;
-  p.rings = new int(0);  // never freed: the piece lives until exit
   if ((e = hipMemAddressReserve((void**)&p.home, bytes, va_align(bytes, gran), nullptr, 0)) != hipSuccess) {
     (void)hipMemRelease(p.h);  // never mapped: safe to give back
     return e;
@@ -198,6 +200,8 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
     (void)hipMemRelease(p.h);
     return e;
   }
+  p.rings = new int(0);  // freed with the piece (ffmp_ring_pool_trim) or never
+  p.maps = new std::vector<char*>(1, p.home);
   *out = p;
   return hipSuccess;
 }
@@ -298,15 +302,14 @@ bool room_for(size_t bytes) {
 // 6 per position), then fresh pieces; with a partner, the first piece whose two-stream store
 // probe against the partner bytes written beside it is within 7 % of the best probe seen
 // (after >= 3 probes), else the best of 12.  Pieces held by a ring are never candidates.
-int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
-                  int64_t partner_bytes) {
-  const int32_t device = r->device;
-  std::vector<ffmp_piece> cand, retired;
-  // Retired pieces become reusable only after a device synchronize that follows their
-  // retirement: snapshot (and remove) this device's retired pieces under the lock, THEN
-  // synchronize, then pool exactly that snapshot.  A ring dropped by another thread after the
-  // snapshot (e.g. a DLPack deleter while ctypes has released the GIL) stays retired until the
-  // next call, so its in-flight writes can never land in a piece handed out here.
+// Retired pieces become reusable only after a device synchronize that follows their
+// retirement: snapshot (and remove) this device's retired pieces under the lock, THEN
+// synchronize, then pool exactly that snapshot.  A ring dropped by another thread after the
+// snapshot (e.g. a DLPack deleter while ctypes has released the GIL) stays retired until the
+// next call, so its in-flight writes can never land in a piece handed out (or released) after
+// this.  The caller has made `device` current.
+int drain_retired(int32_t device) {
+  std::vector<ffmp_piece> retired;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (size_t k = 0; k < g_retired.size();) {
@@ -319,15 +322,23 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
     }
   }
   // every launch issued before the snapshot's rings died has finished once this returns
-  // (the caller's DeviceScope made `device` current)
   if (hipDeviceSynchronize() != hipSuccess) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (const ffmp_piece& p : retired) g_retired.push_back(p);
     return fail(FFMP_E_HIP, "ffmp_ring: hipDeviceSynchronize failed");
   }
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (const ffmp_piece& p : retired) g_pieces.push_back(p);
+  return FFMP_OK;
+}
+
+int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need, const char* partner,
+                  int64_t partner_bytes) {
+  const int32_t device = r->device;
+  std::vector<ffmp_piece> cand;
+  if (const int rc = drain_retired(device)) return rc;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (const ffmp_piece& p : retired) g_pieces.push_back(p);
     for (size_t k = 0; k < g_pieces.size();) {
       if (g_pieces[k].device == device && g_pieces[k].bytes == g.piece) {
         cand.push_back(g_pieces[k]);
@@ -456,8 +467,19 @@ int ring_map(ffmp_ring* r, const RingGeom& g) {
     const int slot = v % r->slots;
     for (int j = 0; j < g.per_slot; ++j) {
       const ffmp_piece& p = r->pieces[(size_t)slot * g.per_slot + j];
-      if ((e = map_rw(r->va + (size_t)v * r->stride + (size_t)j * g.piece, g.piece, p.h, r->device)) != hipSuccess)
-        return fail(FFMP_E_HIP, "ffmp_ring: hipMemMap: %s", hipGetErrorString(e));  // never reused
+      char* at = r->va + (size_t)v * r->stride + (size_t)j * g.piece;
+      e = hipMemMap(at, g.piece, 0, p.h, 0);
+      if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        p.maps->push_back(at);  // unmapped only when the piece's memory is released (pool trim)
+      }
+      if (e == hipSuccess) {
+        hipMemAccessDesc acc = {};
+        acc.location = dev_prop(r->device).location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(at, g.piece, &acc, 1);
+      }
+      if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipMemMap: %s", hipGetErrorString(e));  // never reused
     }
   }
   return FFMP_OK;
@@ -571,6 +593,53 @@ int64_t ffmp_ring_pool_bytes(int32_t device) {
     for (const ffmp_piece& p : *v)
       if (p.device == device || device < 0) b += (int64_t)p.bytes;
   return b;
+}
+
+int ffmp_ring_pool_trim(int32_t device, int64_t keep_bytes, int64_t* released) {
+  if (released) *released = 0;
+  if (device < 0) return fail(FFMP_E_ARG, "ffmp_ring_pool_trim: device must be >= 0");
+  DeviceScope scope(device);
+  // pieces of rings dropped while kernels may still write them become pool pieces only after a
+  // device synchronize; their memory is released after that too
+  if (const int rc = drain_retired(device)) return rc;
+  std::vector<ffmp_piece> victims;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    // the pairing references of this device are forgotten too: they are keyed by the partner
+    // plane's address, and a plane allocated later at the same address must not inherit them
+    g_pair_ref.erase(std::remove_if(g_pair_ref.begin(), g_pair_ref.end(),
+                                    [device](const PairRef& p) { return p.device == device; }),
+                     g_pair_ref.end());
+    int64_t kept = 0;
+    for (size_t k = 0; k < g_pieces.size();) {
+      ffmp_piece& p = g_pieces[k];
+      if (p.device != device || kept + (int64_t)p.bytes <= std::max<int64_t>(keep_bytes, 0)) {
+        if (p.device == device) kept += (int64_t)p.bytes;
+        ++k;
+        continue;
+      }
+      victims.push_back(p);
+      g_pieces.erase(g_pieces.begin() + k);
+    }
+  }
+  int rc = FFMP_OK;
+  int64_t freed = 0;
+  for (ffmp_piece& p : victims) {
+    // every mapping (home + the dead rings' slots) goes; the reservations stay, never reused
+    bool ok = true;
+    for (char* at : *p.maps)
+      if (hipMemUnmap(at, p.bytes) != hipSuccess) ok = false;
+    if (ok && hipMemRelease(p.h) == hipSuccess) {
+      freed += (int64_t)p.bytes;
+      delete p.maps;
+      delete p.rings;
+    } else {
+      (void)hipGetLastError();
+      rc = fail(FFMP_E_HIP, "ffmp_ring_pool_trim: unmapping / releasing a %zu-byte piece failed", p.bytes);
+    }
+  }
+  if (released) *released = freed;
+  return rc;
 }
 
 static void dl_delete(DLManagedTensor_* mt) {

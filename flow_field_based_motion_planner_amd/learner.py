@@ -63,8 +63,10 @@ class Brain:
         self.input_channels = int(input_channels)
         self.temporal_maps = bool(temporal_maps)
         if self.temporal_maps:
-            if not 1 <= self.input_channels <= env.frame_window:
-                raise ValueError(f"temporal_maps: input_channels must be in [1, frame_window={env.frame_window}]")
+            if not 1 <= self.input_channels <= env.max_temporal_frames:
+                raise ValueError(f"temporal_maps: input_channels must be in [1, {env.max_temporal_frames}] for this "
+                                 f"env (frame_window={env.frame_window}, ring={env.ring}; a wrapping ring holds "
+                                 f"W - 1 distinct frames)")
         else:
             if self.input_channels == 3 and not env.cfg.flow:
                 raise ValueError("input_channels=3 needs an env with FFMPConfig(flow=True)")

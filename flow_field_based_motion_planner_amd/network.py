@@ -14,10 +14,15 @@ runs on a batch of env tensors already in HBM:
     the reference computes for B = 1 (its acting path) and keeps samples independent.
 
 The linears are library GEMMs (hipBLASLt through torch).  With `mfma=True` and under bfloat16
-autocast (Brain(amp=True)), every convolution + ReLU runs on the hand-written MFMA kernel instead
-of MIOpen (conv_mfma.py, include/ffmp.h ffmp_conv2d_fwd_bf16; conv1's 1-4 map channels with its
-kernel columns folded into channels; the data gradients too; the weight gradients stay MIOpen's):
-the same bf16-operand / fp32-accumulate arithmetic as autocast's conv2d.
+autocast (Brain(amp=True)), every convolution + ReLU runs on the hand-written MFMA kernels instead
+of MIOpen (conv_mfma.py, include/ffmp.h ffmp_conv2d_fwd_bf16 / ffmp_conv2d_wgrad_bf16: the
+forward, the data gradient and the weight gradient; conv1's 1-4 map channels with its kernel
+columns folded into channels, its input gradient — never needed by the Network — MIOpen's):
+bf16 operands and fp32 accumulation like autocast's conv2d (the bias added in fp32, where
+autocast rounds it to bf16 first).  A layer whose input shape the kernels do not take
+(conv_mfma.supported / fold_supported with the shape: e.g. 64-channel rows over 16 KiB at
+G >= 191, weight-gradient rows under 8 positions at G 91-97, a batch over 65,535) runs
+F.relu(conv(x)) under autocast instead.
 Input maps must be G x G with G - 90 > 0 (conv k=32,32,8 then conv4 k=8 three times); the
 reference's fc2 (6400 inputs) fixes G = 100, other G size fc2 accordingly.
 """
@@ -59,9 +64,9 @@ class Network(nn.Module):
         """relu(conv(x)): on the MFMA kernel when enabled, under bf16 autocast, for its shapes."""
         if self.mfma and x.is_cuda and torch.is_autocast_enabled("cuda") and \
                 torch.get_autocast_dtype("cuda") == torch.bfloat16:
-            if conv_mfma.supported(conv):
+            if conv_mfma.supported(conv, x.shape):
                 return conv_mfma.conv_relu(conv, x)
-            if conv_mfma.fold_supported(conv):  # conv1: 1 / 2 / 4 map channels
+            if conv_mfma.fold_supported(conv, x.shape):  # conv1: 1 / 2 / 3 / 4 map channels
                 return conv_mfma.fold_conv_relu(conv, x)
         return F.relu(conv(x))
 

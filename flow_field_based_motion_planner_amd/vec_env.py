@@ -170,9 +170,24 @@ class FFMPVec:
                 self._recheck_fused()
             if self.placement is not None and self.ring_meta is not None:
                 self.placement = dict(self.placement, ring=self.ring_meta)
+        self.pool_released_bytes = 0
+        if self.release_pool and self.ring == "seamless":
+            # the pairing candidates this instance did not choose, the rings its relocation /
+            # repair dropped: their memory goes back to the device (addresses stay reserved)
+            torch.cuda.synchronize(self.device)
+            self.pool_released_bytes = _abi.ring_pool_trim(self.device.index, 0)
+            if self.ring_meta is not None:
+                self.ring_meta = dict(self.ring_meta, pool_released_bytes=self.pool_released_bytes)
+                if self.placement is not None and "ring" in self.placement:
+                    self.placement = dict(self.placement, ring=self.ring_meta)
         self._needs_reset = True
 
     # ------------------------------------------------------------------ setup
+    # After construction (and on close) the frame-ring pieces parked in the process pool — pairing
+    # candidates not chosen, rings dropped by the relocation / slot repair — are released
+    # (ffmp_ring_pool_trim): at C3 they were ~65 GB beside the instance's 77 GB (round 3).
+    release_pool = True
+
     OBS_FORMATS = {"f32": (_abi.OBS_F32, torch.float32, torch.float32),
                    "u8f16": (_abi.OBS_U8F16, torch.uint8, torch.float16)}
     _ARENA_ALIGN = 2 << 20
@@ -882,6 +897,13 @@ class FFMPVec:
             # guaranteed to be clamped away
             self._hist_from_reset = False
 
+    @property
+    def max_temporal_frames(self) -> int:
+        """The largest k temporal_maps(k) can serve at every step: W for the seamless ring and the
+        contiguous pair, W - 1 for the wrapping ring (its wrap re-rasters the newest frame into slot 0,
+        so after the first wrap it holds W - 1 distinct frames)."""
+        return self.frame_window - 1 if self.ring == "wrap" else self.frame_window
+
     def temporal_maps(self, k: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """make_temporal_maps (src/train.py:474-486) over the last k frames: (N, k, G, G), oldest
         first, each env's lags clamped to its episode start (is_first refills the reference's
@@ -894,9 +916,11 @@ class FFMPVec:
             raise ValueError("k must be >= 1")
         if k <= 2 and out is None:
             return self.state_m[:, 2 - k:]
-        if k > self.frame_window or k > _abi.MAX_SERIES:
-            raise ValueError(f"temporal_maps({k}) needs frame_window >= {k} (this env keeps {self.frame_window}; "
-                             f"at most {_abi.MAX_SERIES})")
+        if k > self.max_temporal_frames or k > _abi.MAX_SERIES:
+            raise ValueError(f"temporal_maps({k}) needs at most {self.max_temporal_frames} frames here "
+                             f"(frame_window={self.frame_window}, ring={self.ring}: a wrapping ring re-rasters "
+                             f"its newest frame into slot 0 and keeps W - 1 distinct frames; at most "
+                             f"{_abi.MAX_SERIES})")
         if self._needs_reset:
             raise RuntimeError("call reset() before temporal_maps()")
         N, G = self.num_envs, self.cfg.grid
@@ -1187,8 +1211,13 @@ class FFMPVec:
         self._state_c = self._obs_c = self._out_c = None
         self._slices = []
         self._arena_buf = None
-        self._ring = None  # the seamless ring's pieces return to the process pool
+        had_ring = self.ring == "seamless"
+        self._ring = None  # the seamless ring's pieces return to the process pool ...
         torch.cuda.empty_cache()
+        if had_ring and self.release_pool:
+            import gc
+            gc.collect()  # ... once the last tensor view of the ring is gone
+            _abi.ring_pool_trim(self.device.index, 0)  # ... and their memory to the device
 
     _closed = False
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 5
+#define FFMP_ABI_VERSION 6
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -317,6 +317,15 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
 int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t batch, int32_t h, int32_t wd, int32_t c,
                            int32_t kh, int32_t kw, int32_t n, int32_t dx, int32_t chunks, void* stream);
 
+/* Would ffmp_conv2d_fwd_bf16 (kind 0; with pad > 0 the data-gradient form) or
+ * ffmp_conv2d_wgrad_bf16 (kind 1; pad ignored) accept this shape?  Runs every check of the launch
+ * (channels, batch <= 65535, 16 KiB input rows, the LDS ring / stage, wgrad rows of >= 8
+ * positions) and launches nothing.  FFMP_OK, or FFMP_E_ARG with the reason in ffmp_last_error().
+ * The learner asks before it routes a convolution to the matrix-core kernels, and keeps the
+ * library convolution for shapes outside them (src/train.py:231-303 at any map size). */
+int ffmp_conv2d_check(int32_t kind, int32_t batch, int32_t h, int32_t wd, int32_t c, int32_t kh, int32_t kw,
+                      int32_t n, int32_t pad, int32_t dx);
+
 /* Episode bookkeeping of the training loop, batched (one record per env, device memory).
  * Per env and per ffmp_episode_update, exactly as src/train.py:579-682 does per iteration:
  *   reach window  <- is_goal (last `window` flags, window <= 64; REACH_MEMORY_CAPACITY = 10)
@@ -396,7 +405,8 @@ int ffmp_temporal_maps(int64_t n, const void* frames, const int64_t* lag_offset,
  * ffmp_ring_destroy drops the creator's reference.  Nothing is ever unmapped while the process
  * runs (ROCm 7 can resolve a reused, re-mapped VMM address to the old allocation — see
  * ffmp_kernels.hip): once a ring's last reference is gone its pieces return to a process-wide
- * pool that later rings draw from.  ffmp_ring_pool_bytes: pooled bytes (device < 0: all).
+ * pool that later rings draw from (or whose memory ffmp_ring_pool_trim gives back, keeping the
+ * addresses reserved).  ffmp_ring_pool_bytes: pooled bytes (device < 0: all).
  * ffmp_ring_info: out[0..4] = pieces, fresh pieces allocated, pairing probes, min and max
  * probe GB/s of the chosen pieces (0 without a partner); with cap >= 6 also out[5] = the partner
  * byte ratio fixed at create (1: float32 frames beside a float32 plane, 2: uint8 frames beside a
@@ -417,6 +427,19 @@ int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partn
 int ffmp_ring_destroy(ffmp_ring_t* ring);
 int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap);
 int64_t ffmp_ring_pool_bytes(int32_t device);
+/* Give back the physical memory of pooled pieces of `device` beyond the first keep_bytes
+ * (0: all of them): after a device synchronize (pieces of rings dropped while kernels may still
+ * write them are drained first), every mapping of such a piece — its home mapping and the slots
+ * of the dead rings that held it — is unmapped and its handle released.  The address ranges
+ * stay reserved until exit, so no later mapping is ever placed at an address that once held
+ * another allocation (the stale-resolution hazard above).  Rings still alive are untouched.
+ * The device's pairing references (the best probe seen per partner plane, keyed by the plane's
+ * address) are forgotten as well, so a plane allocated later at a freed plane's address starts
+ * its own.  *released (optional) = bytes given back.  Returns 0, FFMP_E_ARG or FFMP_E_HIP.
+ * (FFMPVec calls it after construction and on close: an instance's unchosen pairing candidates
+ * and the pieces of rings it dropped go back to the device.)  Replaces no reference interface:
+ * the reference keeps its 2-frame stack as a host NumPy array (src/train.py:474-486). */
+int ffmp_ring_pool_trim(int32_t device, int64_t keep_bytes, int64_t* released);
 /* A dlpack.h (v0.8) DLManagedTensor* of `bits` elements (8: uint8, 16/32/64: float) over `data` (element strides,
  * ndim <= 8), for consumers that take DLPack (torch.utils.dlpack.from_dlpack, CuPy, JAX).
  * Its deleter frees it and, when `owner` is a ring, drops the reference it took on it: a ring

@@ -25,7 +25,7 @@ def pytest_configure(config):
 # process parks the pieces of every frame ring it creates for reuse and never unmaps them
 # (DESIGN §4), so late in the session a child (or a placement retry) would find less free HBM than
 # bench.py does on a fresh box.
-EARLY_MODULES = ("test_gpu_timed_path", "test_gpu_distributed")
+EARLY_MODULES = ("test_gpu_timed_path", "test_gpu_distributed", "test_gpu_rank_shard")
 EARLY_TESTS = ("test_partner_relocation_keeps_a_consistent_env",)
 
 

@@ -42,3 +42,27 @@ def test_c3_within_budget_beside_a_learner():
     assert env.hbm_bytes() <= budget
     env.close()
     lenv.close()
+
+
+def test_default_c3_parks_no_hbm():
+    """With default arguments the metric's instance holds what it uses: the pairing candidates it did
+    not choose and the rings its relocation / repair dropped are released after construction
+    (ffmp_ring_pool_trim), so the device's HBM in use grows by at most 10 % more than hbm_bytes()
+    (round 3: 124 fresh 1 GiB pieces to use 64, ~65 GB parked beside 77 GB).  And on close() its own
+    ring's memory goes back too."""
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(0)
+    env = FFMPVec(32768, preset("C3", seed=9), device="cuda:0")
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(0)
+    grew, held = free0 - free1, env.hbm_bytes()
+    assert env.ring == "seamless" and env.frame_window == 8
+    assert grew - held <= 0.10 * held, (grew, held, env.ring_meta)
+    assert env._ring.info()["pieces_new"] >= 64  # it did pair (and may have probed extra pieces)
+    env.reset()
+    env.step(torch.zeros(32768, dtype=torch.int64, device="cuda:0"))
+    env.close()
+    torch.cuda.synchronize()
+    free2, _ = torch.cuda.mem_get_info(0)
+    assert free0 - free2 <= 0.02 * held, (free0, free2, held)

@@ -177,3 +177,37 @@ def test_temporal_maps_input(amp):
     assert a.shape == (32,) and int(a.max()) < 28
     with pytest.raises(ValueError):
         Brain(env, capacity=256, input_channels=5, temporal_maps=True)  # more frames than the window
+
+
+def test_amp_at_a_grid_outside_the_kernels_falls_back_per_layer():
+    """Brain(amp=True) at G = 96 (the reference's Network accepts G > 90): the third conv4's weight
+    gradient would have output rows of 6 < 8 positions, which the MFMA weight-gradient kernel does
+    not take (ffmp_conv2d_check) — that layer runs F.relu(conv(x)) under autocast, the others stay
+    on the matrix-core kernels, and the update completes (it raised FFMPBackendError before)."""
+    from flow_field_based_motion_planner_amd import conv_mfma
+    cfg = FFMPConfig(grid=96, n_obst=4, n_beams=64, moving=True, max_steps=6, seed=32)
+    env = FFMPVec(32, cfg, device=DEV, keep_terminal=True)
+    env.reset()
+    b16 = Brain(env, capacity=128, batch_size=32, seed=5, amp=True)
+    b32 = Brain(env, capacity=128, batch_size=32, seed=5)
+    b16.memory = b32.memory
+    _fill(b32, env, 2)
+    calls = []
+    real = conv_mfma.conv_relu
+
+    def counting(conv, x):
+        calls.append(tuple(x.shape))
+        return real(conv, x)
+
+    conv_mfma.conv_relu = counting
+    try:
+        idx = torch.arange(32, device=DEV)
+        l16 = b16.replay(index=idx)
+        l32 = b32.replay(index=idx)
+    finally:
+        conv_mfma.conv_relu = real
+    assert torch.isfinite(l16)
+    torch.testing.assert_close(l16, l32, rtol=5e-2, atol=5e-3)
+    sides = sorted({s[2] for s in calls})
+    assert {65, 34, 27, 20} <= set(sides) and 13 not in sides, sides  # conv2, conv3, conv4 x2 on MFMA
+    assert not conv_mfma.supported(b16.main_q_network.conv4, (32, 64, 13, 13))

@@ -219,3 +219,54 @@ def test_pair_probe_stays_inside_a_compact_partner_and_rebuild_keeps_the_scale()
     t[3, :4].fill_(7)  # the alias slot still maps slot 0
     torch.cuda.synchronize()
     assert int(t[0, :4].sum()) == 7 * 4 * G * G
+
+
+def test_pool_trim_gives_memory_back_and_later_rings_see_their_writes():
+    """ffmp_ring_pool_trim: the pooled pieces' memory goes back to the device (every mapping of
+    them unmapped, the address ranges kept reserved), and rings built afterwards — at fresh
+    addresses — read back exactly what kernels and host copies wrote (the stale-resolution hazard
+    of a REUSED address, tools/ring_reuse_probe.hip, cannot arise: no address is reused)."""
+    lib = _abi.load()
+    _abi.ring_pool_trim(DEV, 0)
+    assert lib.ffmp_ring_pool_bytes(DEV) == 0
+    shape = (64, 1024, 1024)  # 256 MiB slots, one piece each
+    rings = [_abi.SeamlessRing(DEV, shape, 4) for _ in range(2)]
+    rings[1].rebuild(0b0011)  # the replaced pieces stay held by the old ring until it is dropped
+    rings[1].drop_previous()
+    stride = rings[0].slot_stride
+    for r in rings:
+        _fill(r.tensor, 4)
+    del r
+    rings = None
+    gc.collect()
+    pooled = lib.ffmp_ring_pool_bytes(DEV)
+    assert pooled >= 8 * stride
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(DEV)
+    released = _abi.ring_pool_trim(DEV, 0)
+    free1, _ = torch.cuda.mem_get_info(DEV)
+    assert released == pooled and lib.ffmp_ring_pool_bytes(DEV) == 0
+    assert free1 - free0 >= 0.95 * released, (free0, free1, released)
+    # keep_bytes: the first pieces up to it stay pooled
+    a = _abi.SeamlessRing(DEV, shape, 3)
+    del a
+    gc.collect()
+    assert _abi.ring_pool_trim(DEV, stride) == 2 * stride and lib.ffmp_ring_pool_bytes(DEV) == stride
+    # new rings after the release: kernel writes, host-to-device copies and the alias all land
+    for k in range(3):
+        r = _abi.SeamlessRing(DEV, shape, 3)
+        t = r.tensor
+        for i in range(3):
+            t[i].fill_(float(10 * k + i))
+        torch.cuda.synchronize()
+        host = t[:4].cpu()  # the D2H copy is what returned an old ring's bytes at a reused address
+        for i in range(3):
+            assert float(host[i].min()) == float(host[i].max()) == float(10 * k + i), (k, i)
+        assert torch.equal(host[3], host[0])
+        pattern = torch.arange(shape[1] * shape[2], dtype=torch.float32).view(shape[1:])
+        t[1, 5].copy_(pattern)
+        torch.cuda.synchronize()
+        assert torch.equal(t[1, 5].cpu(), pattern)
+        del t, r, host
+        gc.collect()
+    _abi.ring_pool_trim(DEV, 0)

@@ -46,8 +46,13 @@ def test_temporal_maps_match_reference_stack(window, seamless, fmt):
     ref = OracleVecEnv(CFG, n)
     env.reset()
     ref.reset()
-    # a wrapping ring keeps W - 1 frames once it has wrapped
+    # a wrapping ring keeps W - 1 frames once it has wrapped: k = W is refused up front,
+    # not after the first wrap
     ks = [k for k in range(1, window + 1) if window == 2 or seamless or k < window]
+    assert env.max_temporal_frames == max(ks)
+    if env.ring == "wrap":
+        with pytest.raises(ValueError, match="wrapping ring"):
+            env.temporal_maps(window)
     stacks = _stacks(ref, ks)
     _push(stacks, ref, np.ones(n, bool))
     _check(env, stacks, "reset")

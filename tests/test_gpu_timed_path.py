@@ -2,7 +2,10 @@
 
 bench.py times C3 (32,768 envs, 256^2, 16 moving discs, 180 beams) through the seamless W = 8
 frame ring paired with the potential plane and the autotuned launch (one-launch
-step_raster_kernel with flags 37 on the round-2 boxes).  tests/timed_path_check.py builds that
+step_raster_kernel with flags 37 on the round-2 boxes; the two-launch step with the newest-only
+raster shape (4096, NT|XCD|TILE4) on the round-3 driver box).  Every one-launch flag set AND every
+two-launch raster shape the autotune may pick runs here, so a candidate added later cannot reach
+a bench line without this full-size check.  tests/timed_path_check.py builds that
 instance the way bench.py does, rebuilds two of its slots, and steps every env through every
 launch kind the autotune may pick — >= W + 2 steps, so every physical slot incl. the alias slot
 is written and then read as the older frame — comparing ALL envs with the C oracle after the
@@ -26,7 +29,15 @@ def _run(fmt: str) -> dict:
     import torch
     torch.cuda.empty_cache()  # this process's cached blocks back to the device for the child
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tests", "timed_path_check.py"), "--obs-format", fmt]
-    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900)
+    out_dir = os.environ.get("FFMP_TIMED_PATH_OUT")  # keep the child's summary + log (profiles/ evidence)
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        cmd += ["--out", os.path.join(out_dir, f"timed_path_{fmt}.json")]
+        with open(os.path.join(out_dir, f"timed_path_{fmt}.log"), "w") as log:
+            p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=log, text=True, timeout=900)
+        p.stderr = open(os.path.join(out_dir, f"timed_path_{fmt}.log")).read()
+    else:
+        p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, f"exit {p.returncode}\nstdout:\n{p.stdout[-3000:]}\nstderr:\n{p.stderr[-6000:]}"
     out = json.loads(lines[-1])
@@ -44,9 +55,16 @@ def test_timed_path_full_size_bit_exact(fmt):
     assert set(out["slots_written"][:-1]) == set(range(W)), out["slots_written"]
     assert out["truncations"] >= out["n_envs"]   # max_steps 6: every env truncated, mid-ring
     assert out["resets"] > out["n_envs"] and out["collisions"] > 0  # plus single-env resets
-    if fmt == "f32":  # every one-launch flag set the autotune can choose was run
-        from flow_field_based_motion_planner_amd.vec_env import FFMPVec
-        used = {f for kind, f in out["launches"] if kind == "fused"}
-        assert used == set(FFMPVec.FUSED_FLAGS) and {37, 33} <= used
+    # every launch the autotune can choose for this layout was run: each one-launch flag set and
+    # each two-launch raster shape (the bench's choice among them: BENCH_r03 (4096, 37))
+    from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+    fused = FFMPVec.FUSED_FLAGS if fmt == "f32" else FFMPVec.COMPACT_FUSED_FLAGS
+    shapes = FFMPVec.RASTER_SHAPES if fmt == "f32" else FFMPVec.COMPACT_SHAPES
+    used_fused = {f for kind, f in out["launches"] if kind == "fused"}
+    used_two = {tuple(s) for kind, s in out["launches"] if kind == "two"}
+    assert used_fused == set(fused), sorted(set(fused) - used_fused)
+    assert used_two >= set(shapes), sorted(set(shapes) - used_two)
+    if fmt == "f32":
+        assert {37, 33} <= used_fused and (4096, 37) in used_two
     # the float outputs were within tolerance; report how many were not bit-identical
     print("not bit-identical:", out["not_bit_identical"], "in", out["seconds"], "s")

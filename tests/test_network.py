@@ -86,3 +86,23 @@ def test_map_channels_options():
         map_channels(sm, None, 3)
     with pytest.raises(ValueError):
         map_channels(sm, fl, 12)
+
+
+def test_mfma_support_follows_the_kernels_shape_limits():
+    """conv_mfma.supported / fold_supported with the input shape ask the library's own launch checks
+    (include/ffmp.h ffmp_conv2d_check, no GPU needed): the reference's G = 100 stack is taken whole;
+    64-channel rows over 16 KiB (conv3 at G >= 191), weight-gradient rows under 8 positions (the
+    third conv4 at G = 91-97) and a batch over 65,535 are not, so Network keeps F.relu(conv(x))
+    for exactly those layers."""
+    from flow_field_based_motion_planner_amd import conv_mfma
+    c1, c2 = torch.nn.Conv2d(2, 32, 32), torch.nn.Conv2d(32, 64, 32)
+    c3, c4 = torch.nn.Conv2d(64, 64, 8), torch.nn.Conv2d(64, 64, 8)
+    B = 256
+    assert conv_mfma.fold_supported(c1, (B, 2, 100, 100)) and conv_mfma.supported(c2, (B, 32, 69, 69))
+    assert conv_mfma.supported(c3, (B, 64, 38, 38))
+    assert all(conv_mfma.supported(c4, (B, 64, s, s)) for s in (31, 24, 17))
+    assert not conv_mfma.supported(c4, (B, 64, 13, 13))      # G = 96: wgrad output rows of 6
+    assert not conv_mfma.supported(c3, (B, 64, 260, 260))    # 64-channel rows of 33 KiB
+    assert not conv_mfma.supported(c2, (70000, 32, 69, 69))  # batch over 65,535
+    assert not conv_mfma.supported(c2, (B, 64, 69, 69))      # channel mismatch
+    assert conv_mfma.supported(c2) and not conv_mfma.supported(c1)  # layer-only form

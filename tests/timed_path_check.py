@@ -13,9 +13,9 @@ kept in place).  One instance, built the way bench.py builds it from a tuning, t
     re-paired; the path the slot repair takes on a box with slow slots);
   * reset, and STEPS steps (>= W + 2, so every physical slot is written as the newest frame and
     then read as the older one, the alias slot included), each step through a different launch
-    the autotune may choose: every one-launch flag set (FFMPVec.FUSED_FLAGS, incl. 37 =
-    NT|XCD|TILE4 and 33 = NT|TILE4, the ones seen chosen on the bench), then two-launch steps with
-    several raster shapes.  max_steps = 6 truncates and auto-resets every env inside a newest-only
+    the autotune may choose: every one-launch flag set (FFMPVec.FUSED_FLAGS), then a two-launch
+    step for EVERY raster shape candidate (FFMPVec.RASTER_SHAPES, incl. (4096, NT|XCD|TILE4), the
+    shape behind the round-3 driver bench).  max_steps = 6 truncates and auto-resets every env inside a newest-only
     launch (both frames of every env written that step); collisions / goals reset single envs on
     other steps;
   * after the reset and after every step, ALL envs are compared in 4,096-env slices: state_m (both
@@ -57,27 +57,27 @@ SLICE = 4096
 SMALL = ("state_g", "state_v", "state_t", "grad", "reward", "done", "is_goal", "collision", "truncated",
          "pose", "goal", "d0", "obst", "obst_r", "t", "episode", "record", "lidar")
 
-# the bench's tuning as seen on the driver's boxes (round 2: fused, flags 37); the per-step plan
-# below overrides the launch of every step anyway
-TUNING = {"f32": {"shape": [16384, _abi.RASTER_NT | _abi.RASTER_TILE4],
-                  "shape_newest": [16384, _abi.RASTER_NT | _abi.RASTER_TILE4],
-                  "fused": True, "fused_flags": _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4},
-          "u8f16": {"shape": [65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW],
-                    "shape_newest": [65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_NARROW],
-                    "fused": False, "fused_flags": _abi.RASTER_NT | _abi.RASTER_TILE16}}
+# the bench's tuning as the driver's round-3 box chose it (BENCH_r03.json raster_autotune: two-launch
+# step, newest-only raster (4096, NT|XCD|TILE4) = flags 37); the per-step plan below overrides the
+# launch of every step anyway
+TUNING = {"f32": {"shape": [4096, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4],
+                  "shape_newest": [4096, _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4],
+                  "fused": False, "fused_flags": _abi.RASTER_NT | _abi.RASTER_XCD | _abi.RASTER_TILE4},
+          "u8f16": {"shape": [65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8],
+                    "shape_newest": [65536, _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8],
+                    "fused": False, "fused_flags": _abi.RASTER_NT | _abi.RASTER_TILE4 | _abi.RASTER_MID8}}
 
 
 def launch_plan(fmt: str):
-    """(fused, flags-or-shape) per step: every one-launch flag set the autotune may pick, then
-    two-launch steps with raster shapes from the autotune's candidate list."""
+    """(fused, flags-or-shape) per step: EVERY launch the autotune may pick for this layout — each
+    one-launch flag set (FUSED_FLAGS / COMPACT_FUSED_FLAGS), then a two-launch step for each raster
+    shape candidate (RASTER_SHAPES / COMPACT_SHAPES) — so that the shape behind any bench line,
+    including candidates added later, has run over the whole ring at full size."""
     if fmt == "f32":
-        fused = list(FFMPVec.FUSED_FLAGS)
-        two = [(16384, _abi.RASTER_NT | _abi.RASTER_TILE4), (4096, _abi.RASTER_PLAIN),
-               (8192, _abi.RASTER_NT | _abi.RASTER_XCD), (2048, _abi.RASTER_NT | _abi.RASTER_TILE4)]
+        fused, two = FFMPVec.FUSED_FLAGS, FFMPVec.RASTER_SHAPES
     else:
-        fused = list(FFMPVec.COMPACT_FUSED_FLAGS)
-        two = list(FFMPVec.COMPACT_SHAPES[:5])
-    return [(True, f) for f in fused] + [(False, s) for s in two]
+        fused, two = FFMPVec.COMPACT_FUSED_FLAGS, FFMPVec.COMPACT_SHAPES
+    return [(True, int(f)) for f in fused] + [(False, (int(c), int(f))) for c, f in two]
 
 
 def small_snapshot(env, sl):
@@ -132,6 +132,7 @@ def main() -> int:
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--seed", type=int, default=33)
     ap.add_argument("--frame-window", type=int, default=8, help="bench.py's W (its automatic choice on a free GPU)")
+    ap.add_argument("--out", default=None, help="also write the JSON summary to this file")
     args = ap.parse_args()
     fmt, n = args.obs_format, args.envs
     t0 = time.time()
@@ -186,8 +187,11 @@ def main() -> int:
     env.check_errors()
     out = {"ok": not problems, "obs_format": fmt, "n_envs": n, "frame_window": W, "ring": env.ring,
            "steps": len(plan), "problems": problems[:20], "ring_meta": env._ring.info(), **stats,
-           "seconds": round(time.time() - t0, 1)}
+           "tuning": TUNING[fmt], "seconds": round(time.time() - t0, 1)}
     print(json.dumps(out), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
     return 0 if not problems else 1
 
 

@@ -6,7 +6,7 @@ mkdir -p $R/gpurun_out/epmc
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE \
   --kernel-include-regex 'env_kernel' --output-format csv -d $R/gpurun_out/epmc/run -o run -- \
-  python3 $R/tools/env_kernel_breakdown.py C3 > $R/gpurun_out/epmc/log.txt 2>&1 || exit 1
+  python3 $R/tools/env_kernel_breakdown.py --preset C3 base > $R/gpurun_out/epmc/log.txt 2>&1 || exit 1
 cd $R && python3 - <<'PY'
 import csv, glob, collections
 f = sorted(glob.glob("gpurun_out/epmc/run/**/run_counter_collection.csv", recursive=True))[-1]

@@ -366,9 +366,20 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x
 
 // CH beams of one lane at a time (beams l0, l0 + lpe, ..., l0 + (CH-1) lpe): the disc loop is
 // outermost, so each disc's four LDS operands are read once per CH beams and the CH beams' tests
-// are independent chains.  Every beam sees exactly lidar_beam's operations in lidar_beam's order
-// (discs in ascending k, then the walls), so every range is bit-identical to it.
+// are independent chains.  Every beam's range is the minimum of the same values lidar_beam
+// computes — h = tp - sqrt(r2 - perp) of each disc with tp > 0 and perp <= r2, kept if h <= L,
+// then the walls — so every range is bit-identical to it (a minimum does not depend on the
+// order its candidates arrive in, and h is never -0).
+// FFMP_LIDAR_DEFER (round 4): a beam's disc candidate is held as (tp, r2 - perp) and its square
+// root taken only when a second candidate arrives for the same beam or after the disc loop.  A
+// wave executes the square root of a candidate branch whenever ANY of its lanes has one: with
+// the root inside the loop that was most disc iterations (a disc is hit by a few of 180 beams,
+// but 64 lanes x CH beams see many discs); deferred, it is CH roots per chunk plus the rare
+// beams that meet two discs.
 // f(l, range) for every beam l < n_beams of this lane.
+#ifndef FFMP_LIDAR_DEFER
+#define FFMP_LIDAR_DEFER 0
+#endif
 template <int CH, class F>
 FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane, int lpe, double x, double y,
                           double c, double s, const double* rxa, const double* rya, const double* rra,
@@ -379,6 +390,9 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
   const double W = cfg.world_half, L = cfg.lidar_max;
   for (int l0 = lane; l0 < nb; l0 += CH * lpe) {
     double dirx[CH], diry[CH], best[CH];
+#if FFMP_LIDAR_DEFER
+    double pt[CH], pq[CH];  // pending candidate: tp and r2 - perp (pq < 0: none)
+#endif
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const int l = l0 + j * lpe;
@@ -386,6 +400,10 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
       dirx[j] = c * b.x - s * b.y;
       diry[j] = s * b.x + c * b.y;
       best[j] = inf;
+#if FFMP_LIDAR_DEFER
+      pt[j] = 0.0;
+      pq[j] = -1.0;
+#endif
     }
     if (!sc.inside) {
       for (uint64_t m = sc.mask; m; m &= m - 1) {
@@ -399,8 +417,17 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
           if (tp > 0.0) {
             const double perp = rr - tp * tp;
             if (perp <= r2) {
+#if FFMP_LIDAR_DEFER
+              if (pq[j] >= 0.0) {  // a second candidate for this beam: settle the first
+                const double h = pt[j] - sqrt(pq[j]);
+                if (h <= L && h < best[j]) best[j] = h;
+              }
+              pt[j] = tp;
+              pq[j] = r2 - perp;  // >= 0: perp <= r2
+#else
               const double h = tp - sqrt(r2 - perp);
               if (h <= L && h < best[j]) best[j] = h;
+#endif
             }
           }
         }
@@ -409,6 +436,12 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
       for (int j = 0; j < CH; ++j) {
         const double dx = dirx[j], dy = diry[j];
         double bj = best[j];
+#if FFMP_LIDAR_DEFER
+        if (pq[j] >= 0.0) {
+          const double h = pt[j] - sqrt(pq[j]);
+          if (h <= L && h < bj) bj = h;
+        }
+#endif
         if (dx > 0.0) { if (sc.wxp && wall_in_reach(W - x, dx, L)) { const double h = (W - x) / dx; if (h <= L && h < bj) bj = h; } }
         else if (dx < 0.0) { if (sc.wxn && wall_in_reach(-W - x, dx, L)) { const double h = (-W - x) / dx; if (h <= L && h < bj) bj = h; } }
         if (dy > 0.0) { if (sc.wyp && wall_in_reach(W - y, dy, L)) { const double h = (W - y) / dy; if (h <= L && h < bj) bj = h; } }
@@ -421,6 +454,114 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
       const int l = l0 + j * lpe;
       if (l < nb) f(l, sc.inside ? -inf : best[j]);
     }
+  }
+}
+
+// Order-preserving uint32 key of a float (a < b <=> fkey(a) < fkey(b), NaN aside) for LDS atomic min.
+FFMP_DEV uint32_t fkey(float v) {
+  const uint32_t b = __float_as_uint(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+FFMP_DEV float funkey(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
+
+// Disc-major lidar (round 4): the same ranges as lidar_beam / trace_beams, from far fewer tests.
+// A disc can return a hit only on the beams within its angular half-width asin(r / |rel|) of its
+// centre's bearing; each of the group's discs (lane k = disc k of the scene mask) lists those
+// beams — bearing and half-width in float32, widened by 1e-3 rad and one beam on each side —, the
+// group's lanes share the (disc, beam) pairs evenly, and each pair runs lidar_beam's exact float64
+// test (tp > 0, perp = |rel|^2 - tp^2 <= r^2, h = tp - sqrt(r^2 - perp), h <= lidar_max), its hit
+// rounded to float32 joining the beam's minimum by an LDS atomic min.  Then each beam adds its wall
+// hits (lidar_beam's tests) and emits.  Identical ranges:
+//  * every pair lidar_beam would accept is tested: off the list, a beam's angle to the centre exceeds
+//    asin(r/|rel|) by >= 1e-3 rad (the float32 bearing / width / index errors are ~1e-6 rad), so
+//    exactly perp - r^2 >= |rel|^2 (sin^2(a + 1e-3) - sin^2 a) >= |rel|^2 1e-6, or tp < 0 by >=
+//    |rel| sin(1e-3) past 90 degrees — margins ~10^8 times the float64 rounding of tp and perp;
+//    a disc with r^2 / |rel|^2 >= 0.98 lists every beam;
+//  * float32 rounding is monotone, so the minimum of the rounded hits (discs and walls) is the
+//    rounded minimum lidar_beam returns, and `h <= lidar_max` is decided in float64 per hit as there;
+//    h is never -0 (x - x = +0), so the minimum is the same value whatever order the hits arrive in.
+// Relies on the beam layout of ffmp_cfg_t.beam_cs (angle -pi + l 2pi/L).  lane / lpe: the env's
+// group; s_key: the env's L uint32 (LDS), s_pref / s_lo: its lpe ints each (LDS).  Every lane of
+// the group calls it (shuffles).  f(l, range) for every beam l.
+template <class F>
+FFMP_DEV void trace_discs(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane, int lpe, double x, double y,
+                          double c, double s, const double* rxa, const double* rya, const double* rra,
+                          const double* r2a, uint32_t* s_key, int* s_pref, int* s_lo, F&& f) {
+  const int nb = cfg.n_beams;
+  if (nb <= 0) return;
+  const double2* bt = reinterpret_cast<const double2*>(cfg.beam_cs);
+  if (sc.inside) {
+    for (int l = lane; l < nb; l += lpe) f(l, -__builtin_inf());
+    return;
+  }
+  const double W = cfg.world_half, L = cfg.lidar_max;
+  for (int l = lane; l < nb; l += lpe) s_key[l] = fkey(__builtin_inff());
+  // this lane's disc: its beams [lo, lo + cnt) (mod L)
+  int lo = 0, cnt = 0;
+  if ((sc.mask >> lane) & 1ull) {
+    const double rx = rxa[lane], ry = rya[lane];
+    const float q = (float)(r2a[lane] / rra[lane]);  // sin^2 of the half-width
+    if (!(q < 0.98f)) {
+      cnt = nb;
+    } else {
+      const float ex = (float)(c * rx + s * ry), ey = (float)(c * ry - s * rx);  // the centre, robot frame
+      const float th = atan2f(ey, ex);
+      const float half = asinf(sqrtf(q)) + 1e-3f;
+      const float per = (float)nb * 0.159154943f;  // beams per radian
+      lo = (int)floorf((th - half + 3.14159265f) * per) - 1;
+      const int hi = (int)ceilf((th + half + 3.14159265f) * per) + 1;
+      cnt = min(hi - lo + 1, nb);
+      lo %= nb;
+      if (lo < 0) lo += nb;
+    }
+  }
+  int incl = cnt;  // inclusive prefix over the group
+  for (int o = 1; o < lpe; o <<= 1) {
+    const int v = __shfl_up(incl, o, lpe);
+    if (lane >= o) incl += v;
+  }
+  const int total = __shfl(incl, lpe - 1, lpe);
+  s_pref[lane] = incl;
+  s_lo[lane] = lo;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int p = lane; p < total; p += lpe) {
+    int k = 0;  // the disc of pair p: the first lane whose inclusive count exceeds p
+    for (int step = lpe >> 1; step > 0; step >>= 1)
+      if (s_pref[k + step - 1] <= p) k += step;
+    int l = s_lo[k] + (p - (k ? s_pref[k - 1] : 0));
+    if (l >= nb) l -= nb;
+    const double2 b = bt[l];
+    const double dirx = c * b.x - s * b.y;
+    const double diry = s * b.x + c * b.y;
+    const double tp = rxa[k] * dirx + rya[k] * diry;
+    if (tp > 0.0) {
+      const double perp = rra[k] - tp * tp;
+      const double r2 = r2a[k];
+      if (perp <= r2) {
+        const double h = tp - sqrt(r2 - perp);
+        if (h <= L) atomicMin(&s_key[l], fkey((float)h));
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool walls = sc.wxp || sc.wxn || sc.wyp || sc.wyn;
+  for (int l = lane; l < nb; l += lpe) {
+    float r = funkey(s_key[l]);
+    if (walls) {
+      const double2 b = bt[l];
+      const double dx = c * b.x - s * b.y, dy = s * b.x + c * b.y;
+      double bj = __builtin_inf();
+      if (dx > 0.0) { if (sc.wxp && wall_in_reach(W - x, dx, L)) { const double h = (W - x) / dx; if (h <= L && h < bj) bj = h; } }
+      else if (dx < 0.0) { if (sc.wxn && wall_in_reach(-W - x, dx, L)) { const double h = (-W - x) / dx; if (h <= L && h < bj) bj = h; } }
+      if (dy > 0.0) { if (sc.wyp && wall_in_reach(W - y, dy, L)) { const double h = (W - y) / dy; if (h <= L && h < bj) bj = h; } }
+      else if (dy < 0.0) { if (sc.wyn && wall_in_reach(-W - y, dy, L)) { const double h = (-W - y) / dy; if (h <= L && h < bj) bj = h; } }
+      r = fminf(r, (float)bj);
+    }
+    f(l, (double)r);
   }
 }
 

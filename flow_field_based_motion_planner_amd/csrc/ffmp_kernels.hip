@@ -218,8 +218,26 @@ FFMP_DEV void for_beams(const ffmp_cfg_t& cfg, int lane, int lpe, double2 b, F&&
 // load, measured): read in the footprint loop itself, one dependent round trip per offset made the
 // footprint 16 us of a C2 env step (profiles/r02_env_chain.txt); staged here, the loads of a wave
 // overlap each other and the state loads.
-FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, int2* s_foot) {
-  for (int f = (int)(threadIdx.x & 63); f < cfg.n_foot; f += 64) s_foot[f] = make_int2(cfg.foot_di[f], cfg.foot_dj[f]);
+// The footprint cells' ego coordinates do not depend on the env (the robot is cell (G/2, G/2) of
+// every ego map), so they are staged as floats: cell_coord of each offset, the same float32
+// operations the test made per env and cell (round 4).
+// s_foot[FFMP_MAX_FOOT] gets the cells' extent {max |ex|, max |ey|} (a wave max; every lane of the
+// wave must call this), which lets env_group skip the footprint test where it cannot fire.
+FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, float2* s_foot) {
+  const int ic = cfg.grid / 2;
+  float bx = 0.0f, by = 0.0f;
+  for (int f = (int)(threadIdx.x & 63); f < cfg.n_foot; f += 64) {
+    const float2 c = make_float2(cell_coord(cfg, ic + cfg.foot_di[f]), cell_coord(cfg, ic + cfg.foot_dj[f]));
+    s_foot[f] = c;
+    bx = fmaxf(bx, fabsf(c.x));
+    by = fmaxf(by, fabsf(c.y));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    bx = fmaxf(bx, __shfl_xor(bx, o, 64));
+    by = fmaxf(by, __shfl_xor(by, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) s_foot[FFMP_MAX_FOOT] = make_float2(bx, by);
 }
 
 // LPE lanes per env (16, 32 or 64 >= K): a wave serves 64 / LPE envs, so the per-env scalar
@@ -228,14 +246,15 @@ FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, int2* s_foot) {
 // cells are strided over the group's lanes.
 // One env's step (or reset) by its LPE-lane group: lane = the lane within the group, s_* = the
 // group's LDS slices (FFMP_MAX_OBST entries each).  Used by env_kernel and step_raster_kernel.
-template <int MODE, int LPE, int BCH = FFMP_BEAM_CHUNK>
+template <int MODE, int LPE, int BCH = FFMP_BEAM_CHUNK, bool DL = false>
 FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, int64_t env_offset,
                                                        const int64_t* __restrict__ action, int32_t initial,
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
                                                        const ffmp_out_t& out, int64_t e, int lane, double* s_ox,
                                                        double* s_oy, double* s_or, double* s_orr, float4* s_ecur,
-                                                       float4* s_eprev, const int2* s_foot, float* s_rhdr = nullptr,
-                                                       float2* s_rvel = nullptr) {
+                                                       float4* s_eprev, const float2* s_foot, float* s_rhdr = nullptr,
+                                                       float2* s_rvel = nullptr, uint32_t* s_key = nullptr,
+                                                       int* s_pref = nullptr, int* s_lo = nullptr) {
   static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
   const int K = cfg.n_obst;
   const int L = cfg.n_beams;
@@ -263,8 +282,6 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
   double c0 = 0.0, s0 = 0.0;
   double vlin = 0.0, vang = 0.0;
   float t_obs = 0.0f;
-  bool col = false, goal = false, trunc = false, done = false;
-  double reward = 0.0;
   bool reset_now = (MODE == kEnvMode_Reset);
 
   if (MODE == kEnvMode_Step) {
@@ -305,27 +322,111 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
   FrameHdr hcur = make_hdr(x1, y1, c1, s1);
   FrameHdr hprev = (MODE == kEnvMode_Step) ? make_hdr(x0, y0, c0, s0) : hcur;
 
+  // ---- the env's outputs from its post-step state: field gradient at the robot cell (central
+  // differences), raster record, state write-back, small obs.  Round 4: a stepped env runs this
+  // BEFORE its lidar and collision tests — nothing here depends on them — and an env that then
+  // resets runs it again for its new episode (first = 1) over what it wrote: the lidar's float64
+  // chains no longer keep the whole post-step state live (fewer registers), and the bytes
+  // written are the same. ----
+  auto finish = [&](bool first) {
+    const float2 ge = to_ego(gx, gy, x1, y1, c1, s1);
+    float U = 0.0f;
+    if (lane < 4) {
+      const int di = (lane == 0) ? 1 : (lane == 1) ? -1 : 0;
+      const int dj = (lane == 2) ? 1 : (lane == 3) ? -1 : 0;
+      U = potential_cell(cfg, s_ecur, K, ge.x, ge.y, ic + di, ic + dj);
+    }
+    const float Uxp = __shfl(U, 0, LPE), Uxm = __shfl(U, 1, LPE), Uyp = __shfl(U, 2, LPE),
+                Uym = __shfl(U, 3, LPE);
+    if (lane == 0) {
+      ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
+      ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
+    }
+    const float4 ecur = has_obst ? s_ecur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 eprev = has_obst ? s_eprev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 vel = ego_vel(my, c1, s1);
+    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel,
+                 first ? 1.0f : 0.0f);
+    if (s_rhdr) {  // the one-launch step: the record's header (and velocities) for the block's raster, in LDS
+      if (lane < FFMP_REC_HDR) {
+        const float hv[FFMP_REC_HDR] = {hcur.px, hcur.py, hcur.c, hcur.s, hprev.px, hprev.py, hprev.c, hprev.s,
+                                        ge.x,    ge.y,    first ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        s_rhdr[lane] = hv[lane];
+      }
+      if (s_rvel && has_obst) s_rvel[lane] = make_float2(vel.x, vel.y);
+    }
+    // the terminal state (keep_terminal): the post-step record of a stepped env — also when it
+    // resets below, which rewrites only st.record
+    if (MODE == kEnvMode_Step && !first && st.term_record)
+      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
+    if (has_obst) {
+      double* p = st.obst + (e * K + lane) * 4;
+      p[0] = my.x; p[1] = my.y; p[2] = my.vx; p[3] = my.vy;
+      st.obst_r[e * K + lane] = my.r;
+    }
+    if (lane == 0) {
+      st.pose[e * 3 + 0] = x1; st.pose[e * 3 + 1] = y1; st.pose[e * 3 + 2] = yaw1;
+      st.goal[e * 2 + 0] = gx; st.goal[e * 2 + 1] = gy;
+      st.d0[e] = d0;
+      st.t[e] = t;
+      st.episode[e] = episode;
+      ob.state_v[e * 2 + 0] = (float)vlin;
+      ob.state_v[e * 2 + 1] = (float)vang;
+      ob.state_t[e] = t_obs;
+    }
+  };
+
   if (MODE == kEnvMode_Step) {
     // ---- relative goal (train.py:174-180) ----
     const double dx = gx - x1, dy = gy - y1;
     const double dist = sqrt(dx * dx + dy * dy);
+    if (lane == 0) {
+      // small obs of the post-step state (a reset below overwrites state_g)
+      const float g0 = (float)dist, g1 = (float)pi_to_pi(atan2(dy, dx) - yaw1);
+      ob.state_g[e * 2 + 0] = g0;
+      ob.state_g[e * 2 + 1] = g1;
+      if (st.term_obs) {
+        float* to = st.term_obs + e * 5;
+        to[0] = g0; to[1] = g1; to[2] = (float)vlin; to[3] = (float)vang; to[4] = t_obs;
+      }
+    }
+    finish(false);
+    FFMP_ENV_STAMP(3);
     // ---- collision: footprint on the current occupancy (ffmp.py:85-105) ----
     // (cells in a wave-uniform loop over the offsets staged in LDS by stage_footprint, discs
     // lane-parallel: lane k tests its disc k, lane 0 the walls; the ballot below ORs them:
     // occupied_cell's value for every cell)
+    // (round 4) Most waves skip the loop: with the cells' extent fb = {max |ex|, max |ey|}, a disc
+    // whose centre is farther than r (+ 0.01 % + 1 um) beyond it along x or y contains no cell
+    // (|ex - ox| > r, so (ex - ox)^2 > r^2 after rounding), and a robot farther than the cells' reach
+    // (+ margins) from every wall has no cell outside the world (|c ex - s ey| <= |ex| + |ey|): the
+    // loop would return false.  Collisions are rare, so the test runs only where one is possible.
     bool c_foot = false;
     if (cfg.collide_mode & FFMP_COLLIDE_FOOTPRINT) {
-      for (int f = 0; f < cfg.n_foot; ++f) {
-        const int2 fo = s_foot[f];
-        const float ex = cell_coord(cfg, ic + fo.x), ey = cell_coord(cfg, ic + fo.y);
-        c_foot |= (has_obst && in_disc(ex, ey, ecur1)) || (lane == 0 && outside_world(cfg, hcur, ex, ey));
+      const float2 fb = s_foot[FFMP_MAX_FOOT];
+      const float Wf = cfg.world_half_f * 0.9999f, reach = (fb.x + fb.y) * 1.0001f + 1e-6f;
+      const bool wall = !(fabsf(hcur.px) + reach < Wf && fabsf(hcur.py) + reach < Wf);
+      const float rr = ecur1.w * 1.0001f + 1e-6f;
+      const bool disc = has_obst && !(fabsf(ecur1.x) - fb.x > rr || fabsf(ecur1.y) - fb.y > rr);
+      if (__ballot(disc || (wall && lane == 0)) != 0) {
+        for (int f = 0; f < cfg.n_foot; ++f) {
+          const float2 fc = s_foot[f];
+          const float ex = fc.x, ey = fc.y;
+          c_foot |= (disc && in_disc(ex, ey, ecur1)) || (wall && lane == 0 && outside_world(cfg, hcur, ex, ey));
+        }
       }
     }
     FFMP_ENV_STAMP(7);
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    if constexpr (BCH > 1) {
+    if constexpr (DL) {
+      trace_discs(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo, [&](int l, double r) {
+        const float rf = (float)r;
+        ob.lidar[e * L + l] = rf;
+        c_lidar |= beam_collides(rf, cfg.robot_r);
+      });
+    } else if constexpr (BCH > 1) {
       trace_beams<BCH>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, [&](int l, double r) {
         const float rf = (float)r;
         ob.lidar[e * L + l] = rf;
@@ -341,32 +442,24 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     FFMP_ENV_STAMP(8);
     c_foot = group_ballot(c_foot, LPE) != 0;
     c_lidar = (group_ballot(c_lidar, LPE) != 0) && (cfg.collide_mode & FFMP_COLLIDE_LIDAR);
-    col = c_foot || c_lidar;
     // ---- is_goal / reward / is_done (ffmp.py:120-164), truncation (train.py:607) ----
-    goal = dist < cfg.goal_thr;
-    reward = reward_calc(dist, d0, col, goal);
-    trunc = (cfg.max_steps > 0) && (t >= cfg.max_steps);
-    done = col || goal || trunc;
+    const bool col = c_foot || c_lidar;
+    const bool goal = dist < cfg.goal_thr;
+    const double reward = reward_calc(dist, d0, col, goal);
+    const bool trunc = (cfg.max_steps > 0) && (t >= cfg.max_steps);
+    const bool done = col || goal || trunc;
     reset_now = done && cfg.autoreset;
     if (lane == 0) {
-      // small obs of the post-step state
-      const float g0 = (float)dist, g1 = (float)pi_to_pi(atan2(dy, dx) - yaw1);
-      if (!reset_now) {
-        ob.state_g[e * 2 + 0] = g0;
-        ob.state_g[e * 2 + 1] = g1;
-      }
-      if (st.term_obs) {
-        float* to = st.term_obs + e * 5;
-        to[0] = g0; to[1] = g1; to[2] = (float)vlin; to[3] = (float)vang; to[4] = t_obs;
-      }
+      out.reward[e] = (float)reward;
+      out.done[e] = done;
+      out.is_goal[e] = goal;
+      out.collide[e] = col;
+      out.truncated[e] = trunc;
     }
     FFMP_ENV_STAMP(9);
-    if (reset_now && st.term_record)  // the terminal state, before the reset below overwrites it
-      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev,
-                   to_ego(gx, gy, x1, y1, c1, s1), s_ecur[lane], s_eprev[lane], ego_vel(my, c1, s1), 0.0f);
   }
 
-  FFMP_ENV_STAMP(3);
+  FFMP_ENV_STAMP(4);
   if (reset_now) {
     // ---- episode reset (the external /episode_manager; train.py:559-566) ----
     episode = (MODE == kEnvMode_Reset && initial) ? 0 : episode + 1;
@@ -395,7 +488,10 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
     const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
-    if constexpr (BCH > 1) {
+    if constexpr (DL) {
+      trace_discs(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo,
+                  [&](int l, double r) { ob.lidar[e * L + l] = (float)r; });
+    } else if constexpr (BCH > 1) {
       trace_beams<BCH>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or,
                                    [&](int l, double r) { ob.lidar[e * L + l] = (float)r; });
     } else {
@@ -403,70 +499,19 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
         ob.lidar[e * L + l] = (float)lidar_beam(cfg, sc, x1, y1, c1, s1, b.x, b.y, s_ox, s_oy, s_orr, s_or);
       });
     }
-  }
-
-  FFMP_ENV_STAMP(4);
-  // ---- field-gradient lookup at the robot cell (central differences) ----
-  {
-    const float2 ge = to_ego(gx, gy, x1, y1, c1, s1);
-    float U = 0.0f;
-    if (lane < 4) {
-      const int di = (lane == 0) ? 1 : (lane == 1) ? -1 : 0;
-      const int dj = (lane == 2) ? 1 : (lane == 3) ? -1 : 0;
-      U = potential_cell(cfg, s_ecur, K, ge.x, ge.y, ic + di, ic + dj);
-    }
-    const float Uxp = __shfl(U, 0, LPE), Uxm = __shfl(U, 1, LPE), Uyp = __shfl(U, 2, LPE),
-                Uym = __shfl(U, 3, LPE);
-    if (lane == 0) {
-      ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
-      ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
-    }
-    const float4 ecur = has_obst ? s_ecur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 eprev = has_obst ? s_eprev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 vel = ego_vel(my, c1, s1);
-    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel,
-                 reset_now ? 1.0f : 0.0f);
-    if (s_rhdr) {  // the one-launch step: the record's header (and velocities) for the block's raster, in LDS
-      if (lane < FFMP_REC_HDR) {
-        const float hv[FFMP_REC_HDR] = {hcur.px, hcur.py, hcur.c, hcur.s, hprev.px, hprev.py, hprev.c, hprev.s,
-                                        ge.x,    ge.y,    reset_now ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        s_rhdr[lane] = hv[lane];
-      }
-      if (s_rvel && has_obst) s_rvel[lane] = make_float2(vel.x, vel.y);
-    }
-    if (MODE == kEnvMode_Step && !reset_now && st.term_record)
-      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
-  }
-
-  FFMP_ENV_STAMP(5);
-  // ---- write back state / obs / outputs ----
-  if (has_obst) {
-    double* p = st.obst + (e * K + lane) * 4;
-    p[0] = my.x; p[1] = my.y; p[2] = my.vx; p[3] = my.vy;
-    st.obst_r[e * K + lane] = my.r;
-  }
-  if (lane == 0) {
-    st.pose[e * 3 + 0] = x1; st.pose[e * 3 + 1] = y1; st.pose[e * 3 + 2] = yaw1;
-    st.goal[e * 2 + 0] = gx; st.goal[e * 2 + 1] = gy;
-    st.d0[e] = d0;
-    st.t[e] = t;
-    st.episode[e] = episode;
-    ob.state_v[e * 2 + 0] = (float)vlin;
-    ob.state_v[e * 2 + 1] = (float)vang;
-    ob.state_t[e] = t_obs;
-    if (MODE == kEnvMode_Step) {
-      out.reward[e] = (float)reward;
-      out.done[e] = done;
-      out.is_goal[e] = goal;
-      out.collide[e] = col;
-      out.truncated[e] = trunc;
-    }
+    finish(true);
   }
   FFMP_ENV_STAMP(6);
 }
 
+// FFMP_ENV_WPE: a probe knob (tools/ builds) — ask the compiler for at least this many waves per SIMD
+#ifdef FFMP_ENV_WPE
+#define FFMP_ENV_OCC __attribute__((amdgpu_waves_per_eu(FFMP_ENV_WPE)))
+#else
+#define FFMP_ENV_OCC
+#endif
 template <int MODE, int kEnvWaves, int LPE>
-__global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+__global__ __launch_bounds__(64 * kEnvWaves) FFMP_ENV_OCC void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                  const int64_t* __restrict__ action,
                                                  const uint8_t* __restrict__ mask, int32_t initial,
                                                  ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
@@ -474,7 +519,11 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
   __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
       s_ora[kEnvWaves][FFMP_MAX_OBST], s_orra[kEnvWaves][FFMP_MAX_OBST];
   __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
-  __shared__ int2 s_foota[kEnvWaves][FFMP_MAX_FOOT];
+  __shared__ float2 s_foota[kEnvWaves][FFMP_MAX_FOOT + 1];  // + the cells' extent
+  // the disc-major lidar's per-env beam minima ([wave][env][L] uint32, dynamic: L * 4 bytes per env)
+  // and per-disc pair counts / first beams
+  extern __shared__ uint32_t s_keys[];
+  __shared__ int s_prefa[kEnvWaves][64], s_loa[kEnvWaves][64];
 
   const int wv = threadIdx.x >> 6;
   const int grp = (threadIdx.x & 63) / LPE;
@@ -483,9 +532,11 @@ __global__ __launch_bounds__(64 * kEnvWaves) void env_kernel(ffmp_cfg_t cfg, int
   if (MODE == kEnvMode_Step) stage_footprint(cfg, s_foota[wv]);
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
-  env_group<MODE, LPE>(cfg, env_offset, action, initial, st, ob, out, e, lane, s_oxa[wv] + grp * LPE,
-                       s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_orra[wv] + grp * LPE,
-                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE, s_foota[wv]);
+  env_group<MODE, LPE, FFMP_BEAM_CHUNK, true>(cfg, env_offset, action, initial, st, ob, out, e, lane,
+                       s_oxa[wv] + grp * LPE, s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_orra[wv] + grp * LPE,
+                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE, s_foota[wv], nullptr, nullptr,
+                       s_keys + ((size_t)wv * EPW + grp) * cfg.n_beams, s_prefa[wv] + grp * LPE,
+                       s_loa[wv] + grp * LPE);
 }
 
 // ============================================================================
@@ -1045,7 +1096,7 @@ __global__ __launch_bounds__(256, (kFusedMinWaves<FLOW, FMT>)) void step_raster_
                                                           int32_t tile_log2r) {
   __shared__ double s_ox[FFMP_MAX_OBST], s_oy[FFMP_MAX_OBST], s_or[FFMP_MAX_OBST], s_orr[FFMP_MAX_OBST];
   __shared__ float4 s_ecur[FFMP_MAX_OBST], s_eprev[FFMP_MAX_OBST];
-  __shared__ int2 s_foot[FFMP_MAX_FOOT];
+  __shared__ float2 s_foot[FFMP_MAX_FOOT + 1];  // + the cells' extent
   __shared__ float2 s_vel[FLOW ? FFMP_MAX_OBST : 1];
   __shared__ float s_hdr[FFMP_REC_HDR];
   const int64_t e = logical_block<XCD>();
@@ -1269,7 +1320,8 @@ void launch_env_t(const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const in
                   hipStream_t s) {
   const int64_t per_block = (int64_t)W * (64 / LPE);
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
-  hipLaunchKernelGGL((env_kernel<MODE, W, LPE>), dim3(blocks), dim3(64 * W), 0, s, cfg, n, env_offset, action, mask,
+  const size_t lds = (size_t)W * (64 / LPE) * (size_t)cfg.n_beams * sizeof(uint32_t);  // trace_discs' beam minima
+  hipLaunchKernelGGL((env_kernel<MODE, W, LPE>), dim3(blocks), dim3(64 * W), lds, s, cfg, n, env_offset, action, mask,
                      initial, st, ob, o);
 }
 

@@ -366,20 +366,12 @@ FFMP_DEV double lidar_beam(const ffmp_cfg_t& cfg, const LidarScene& sc, double x
 
 // CH beams of one lane at a time (beams l0, l0 + lpe, ..., l0 + (CH-1) lpe): the disc loop is
 // outermost, so each disc's four LDS operands are read once per CH beams and the CH beams' tests
-// are independent chains.  Every beam's range is the minimum of the same values lidar_beam
-// computes — h = tp - sqrt(r2 - perp) of each disc with tp > 0 and perp <= r2, kept if h <= L,
-// then the walls — so every range is bit-identical to it (a minimum does not depend on the
-// order its candidates arrive in, and h is never -0).
-// FFMP_LIDAR_DEFER (round 4): a beam's disc candidate is held as (tp, r2 - perp) and its square
-// root taken only when a second candidate arrives for the same beam or after the disc loop.  A
-// wave executes the square root of a candidate branch whenever ANY of its lanes has one: with
-// the root inside the loop that was most disc iterations (a disc is hit by a few of 180 beams,
-// but 64 lanes x CH beams see many discs); deferred, it is CH roots per chunk plus the rare
-// beams that meet two discs.
+// are independent chains.  Every beam sees exactly lidar_beam's operations in lidar_beam's order
+// (discs in ascending k, then the walls), so every range is bit-identical to it.  The one-launch
+// step's env phase uses it; the env kernel traces by discs (trace_discs, below).  (Round 4 tried
+// deferring each beam's square root until a second candidate or the loop's end: bit-identical,
+// 1-3 us slower at C3, not kept; profiles/r04_env_kernel.txt.)
 // f(l, range) for every beam l < n_beams of this lane.
-#ifndef FFMP_LIDAR_DEFER
-#define FFMP_LIDAR_DEFER 0
-#endif
 template <int CH, class F>
 FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane, int lpe, double x, double y,
                           double c, double s, const double* rxa, const double* rya, const double* rra,
@@ -390,9 +382,6 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
   const double W = cfg.world_half, L = cfg.lidar_max;
   for (int l0 = lane; l0 < nb; l0 += CH * lpe) {
     double dirx[CH], diry[CH], best[CH];
-#if FFMP_LIDAR_DEFER
-    double pt[CH], pq[CH];  // pending candidate: tp and r2 - perp (pq < 0: none)
-#endif
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const int l = l0 + j * lpe;
@@ -400,10 +389,6 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
       dirx[j] = c * b.x - s * b.y;
       diry[j] = s * b.x + c * b.y;
       best[j] = inf;
-#if FFMP_LIDAR_DEFER
-      pt[j] = 0.0;
-      pq[j] = -1.0;
-#endif
     }
     if (!sc.inside) {
       for (uint64_t m = sc.mask; m; m &= m - 1) {
@@ -417,17 +402,8 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
           if (tp > 0.0) {
             const double perp = rr - tp * tp;
             if (perp <= r2) {
-#if FFMP_LIDAR_DEFER
-              if (pq[j] >= 0.0) {  // a second candidate for this beam: settle the first
-                const double h = pt[j] - sqrt(pq[j]);
-                if (h <= L && h < best[j]) best[j] = h;
-              }
-              pt[j] = tp;
-              pq[j] = r2 - perp;  // >= 0: perp <= r2
-#else
               const double h = tp - sqrt(r2 - perp);
               if (h <= L && h < best[j]) best[j] = h;
-#endif
             }
           }
         }
@@ -436,12 +412,6 @@ FFMP_DEV void trace_beams(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
       for (int j = 0; j < CH; ++j) {
         const double dx = dirx[j], dy = diry[j];
         double bj = best[j];
-#if FFMP_LIDAR_DEFER
-        if (pq[j] >= 0.0) {
-          const double h = pt[j] - sqrt(pq[j]);
-          if (h <= L && h < bj) bj = h;
-        }
-#endif
         if (dx > 0.0) { if (sc.wxp && wall_in_reach(W - x, dx, L)) { const double h = (W - x) / dx; if (h <= L && h < bj) bj = h; } }
         else if (dx < 0.0) { if (sc.wxn && wall_in_reach(-W - x, dx, L)) { const double h = (-W - x) / dx; if (h <= L && h < bj) bj = h; } }
         if (dy > 0.0) { if (sc.wyp && wall_in_reach(W - y, dy, L)) { const double h = (W - y) / dy; if (h <= L && h < bj) bj = h; } }

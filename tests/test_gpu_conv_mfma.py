@@ -35,7 +35,10 @@ def _ref64(xb, wp, bias, pad=0):
     # the row-ring kernel with padding at each tile size (512 / 256 / 128 positions)
     (2, 30, 30, 64, 3, 64, 2), (2, 12, 12, 64, 2, 64, 1), (2, 10, 10, 32, 2, 32, 1),
     # the small-image kernel on data-gradient shapes: conv3's and conv4's (k - 1 = 7 zero cells)
-    (2, 31, 31, 64, 8, 64, 7), (2, 10, 10, 64, 8, 64, 7)])
+    (2, 31, 31, 64, 8, 64, 7), (2, 10, 10, 64, 8, 64, 7),
+    # the 4 x 8 patch kernel of the data gradient (round 4) on ragged outputs: heights not a multiple
+    # of 4, widths not a multiple of 8, patches past the image, each patches-per-workgroup choice
+    (1, 50, 45, 64, 6, 32, 5), (2, 45, 9, 32, 3, 64, 2), (1, 47, 33, 32, 7, 32, 6), (3, 60, 61, 64, 17, 64, 16)])
 def test_conv_fwd_matches_float64(B, H, W, C, K, N, pad):
     g = torch.Generator(device=DEV).manual_seed(B * 1000 + H + K)
     xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)

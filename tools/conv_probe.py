@@ -28,7 +28,8 @@ def timeit(fn, reps=10):
     return e0.elapsed_time(e1) / reps
 
 
-for B in [int(a) for a in (sys.argv[1:] or ["256", "1024"])]:
+MFMA_ONLY = "--mfma-only" in sys.argv  # skip the MIOpen rows (their searches take minutes on a fresh box)
+for B in [int(a) for a in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["256", "1024"])]:
     flop = 2.0 * B * 38 * 38 * 64 * 32 * 32 * 32
     x = torch.relu(torch.randn(B, 32, 69, 69, device=dev)).to(torch.bfloat16)
     w = (torch.randn(64, 32, 32, 32, device=dev) / 181.0).to(torch.bfloat16)
@@ -39,18 +40,21 @@ for B in [int(a) for a in (sys.argv[1:] or ["256", "1024"])]:
     rows = {}
     rows["mfma fwd (bf16 out, relu)"] = timeit(lambda: conv2d_nhwc(xn, wp, bias, relu=True, out_dtype=torch.bfloat16))
     rows["mfma fwd (f32 out)"] = timeit(lambda: conv2d_nhwc(xn, wp, bias))
-    rows["miopen fwd NCHW"] = timeit(lambda: F.conv2d(x, w, bias.to(torch.bfloat16)))
-    rows["miopen fwd NHWC"] = timeit(lambda: F.conv2d(xcl, w.contiguous(memory_format=torch.channels_last),
-                                                      bias.to(torch.bfloat16)))
+    if not MFMA_ONLY:
+        rows["miopen fwd NCHW"] = timeit(lambda: F.conv2d(x, w, bias.to(torch.bfloat16)))
+        rows["miopen fwd NHWC"] = timeit(lambda: F.conv2d(xcl, w.contiguous(memory_format=torch.channels_last),
+                                                          bias.to(torch.bfloat16)))
     gy = torch.randn(B, 64, 38, 38, device=dev).to(torch.bfloat16)
     gn = gy.permute(0, 2, 3, 1).contiguous()
     wd = pack_weight_dgrad(w)
     rows["mfma dgrad (pad 31, bf16 out)"] = timeit(lambda: conv2d_nhwc(gn, wd, None, out_dtype=torch.bfloat16, pad=31))
-    rows["miopen dgrad NCHW"] = timeit(lambda: torch.ops.aten.convolution_backward(
-        gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False]))
+    if not MFMA_ONLY:
+        rows["miopen dgrad NCHW"] = timeit(lambda: torch.ops.aten.convolution_backward(
+            gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False]))
     rows["mfma wgrad"] = timeit(lambda: conv2d_wgrad_nhwc(gn, xn, 32, 32))
-    rows["miopen wgrad NCHW"] = timeit(lambda: torch.ops.aten.convolution_backward(
-        gy, x, w, [64], [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True]))
+    if not MFMA_ONLY:
+        rows["miopen wgrad NCHW"] = timeit(lambda: torch.ops.aten.convolution_backward(
+            gy, x, w, [64], [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True]))
     for k, ms in rows.items():
         print(f"B={B:5d} {k:28s} {ms:8.3f} ms  {flop / ms / 1e9:7.1f} TFLOP/s", flush=True)
     # conv1: 2 -> 32 channels, k = 32, 100^2 -> 69^2 (0.62 GFLOP per sample)
@@ -60,6 +64,8 @@ for B in [int(a) for a in (sys.argv[1:] or ["256", "1024"])]:
     w1f = pack_weight_fold(w1, 16)
     r1 = {"mfma conv1 fold (incl. fold)": timeit(lambda: conv2d_nhwc(fold_input(s0, 16), w1f, None, relu=True,
                                                                       out_dtype=torch.bfloat16, dx=16)),
-          "miopen conv1 fwd NCHW": timeit(lambda: F.conv2d(s0.to(torch.bfloat16), w1.to(torch.bfloat16)))}
+          }
+    if not MFMA_ONLY:
+        r1["miopen conv1 fwd NCHW"] = timeit(lambda: F.conv2d(s0.to(torch.bfloat16), w1.to(torch.bfloat16)))
     for k, ms in r1.items():
         print(f"B={B:5d} {k:28s} {ms:8.3f} ms  {flop1 / ms / 1e9:7.1f} TFLOP/s", flush=True)

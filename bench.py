@@ -361,7 +361,8 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         print("raster ms per launch:", " ".join(f"{x:.3f}" for x in r_ms), file=sys.stderr, flush=True)
     n_full = sum(1 for r in raster_ev if r[4])
     G2 = cfg.grid * cfg.grid
-    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / len(raster_ev) * fb * G2
+    # resets spread evenly over the timed launches
+    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / (K * env.pipeline_slices) * fb * G2
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
@@ -380,7 +381,8 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
                      "kernel": "step_raster_kernel" if env.fused else "raster_kernel",
                      "kernel_ms": sum(r_ms) / len(r_ms),
                      "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
-                     "launches_per_step": len(r_ms) // K, "full_launches": n_full, "timed_resets": resets},
+                     "launches_per_step": env.pipeline_slices, "timed_launches": len(r_ms),
+                     "full_launches": n_full, "timed_resets": resets},
         "raster_ms_per_step": sum(r_ms) / K,
         "step_ms_events": ev_loop[0].elapsed_time(ev_loop[1]) / K,
         "pipeline_slices": env.pipeline_slices,

@@ -370,9 +370,14 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
   };
   int todo = 0;
   for (char n : need) todo += n != 0;
-  // fresh pieces beyond need are the price of pairing (capped under an HBM budget)
+  // fresh pieces beyond need are the price of pairing (capped under an HBM budget).  Round 4: up to
+  // one extra candidate per position (was one per two): with half, the search ran out of fresh
+  // pieces on about half of fresh C3 processes (100 of 100 used) and the last slot's positions took
+  // whatever was left — one slot 20 % slower, the metric -2.5 % (profiles/r04h_slot_repair.txt); the
+  // unchosen pieces go back to the device afterwards (ffmp_ring_pool_trim), and only while
+  // max(8 GiB, 5 %) of HBM stays free (room_for)
   const int32_t extra = ffmp_detail::g_ring_extra.load();
-  const int max_new = todo + (extra > 0 ? extra - 1 : todo / 2 + 4);
+  const int max_new = todo + (extra > 0 ? extra - 1 : todo + 8);
   // best probe seen against this partner plane: the scale "fast" is judged against
   double ref = g.pairing ? pair_ref_get(device, g.scale, partner) : 0.0;
   bool found_fast = false;

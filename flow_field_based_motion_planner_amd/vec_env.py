@@ -485,18 +485,29 @@ class FFMPVec:
 
     # Slot repair (seamless ring).  The pairing probe at ring creation predicts most, not all,
     # slow slot/potential pairings; the step loop itself is the judge: time every slot's
-    # newest-only raster over two ring cycles and rebuild the ring with new pieces for slots
-    # more than SLOW_SLOT above the fastest (ffmp_ring_rebuild), up to REPAIR_ROUNDS times.  A
-    # rebuild re-maps every slot, so only clearly slow slots are worth one.
-    SLOW_SLOT = 1.12
+    # newest-only raster over two ring cycles (after SLOT_WARMUP_CYCLES untimed ones) and rebuild
+    # the ring with new pieces for slots more than SLOW_SLOT above the fastest (ffmp_ring_rebuild),
+    # up to REPAIR_ROUNDS times, keeping the rebuilt ring only if its cycle is faster.  (The 12 %
+    # threshold of rounds 1-3 guarded against rebuilds judged on post-idle timings; with the
+    # warm-up, 6 %: profiles/r04h_slot_repair.txt.)
+    SLOW_SLOT = 1.06
     REPAIR_ROUNDS = 2
     PAIR_SLOTS = True  # build the ring's slots from pieces probed against the potential plane
+
+    # untimed ring cycles before the slot timing: the timing follows host work (construction, a
+    # rebuild's pairing probes) that left the GPU idle, and after such a gap the raster runs slow
+    # for about one ring cycle while the GPU warms up again (profiles/r03b_transient_*.txt); timed
+    # straight after a rebuild, kept slots read 4-7 % slow and good rebuilds were reverted
+    # (profiles/r04h_slot_repair.txt)
+    SLOT_WARMUP_CYCLES = 2
 
     def _slot_ms(self) -> Dict[int, float]:
         """Median newest-only raster ms per physical slot written, over two ring cycles."""
         W = self.frame_window
         self.reset()
         a = torch.full((self.num_envs,), 10, dtype=torch.int64, device=self.device)
+        for _ in range(self.SLOT_WARMUP_CYCLES * W):
+            self.step(a)
         t = []
         for _ in range(2 * W):
             self.step(a, timing=t)

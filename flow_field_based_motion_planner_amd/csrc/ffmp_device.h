@@ -293,17 +293,25 @@ struct LidarScene {
   bool wxp, wxn, wyp, wyn;
 };
 
-// Call from every lane of the env's lane group; its lane k < K holds disc k.
-FFMP_DEV LidarScene lidar_scene(const ffmp_cfg_t& cfg, double x, double y, double ox, double oy, double r,
-                                bool has, int lpe) {
-  const double rx = ox - x, ry = oy - y;
-  const double rr = rx * rx + ry * ry;
-  const bool in = has && (rr <= r * r);
+// Call from every lane of the env's lane group; its lane holds discs k = lane + j lpe (j < DPL),
+// those with k < K real.
+template <int DPL>
+FFMP_DEV LidarScene lidar_scene(const ffmp_cfg_t& cfg, double x, double y, const Obst (&my)[DPL], int lane, int K,
+                                int lpe) {
   const double reach = cfg.lidar_max + kLidarCullMargin;
-  const bool act = has && (in || !(sqrt(rr) - r > reach));
   LidarScene sc;
-  sc.mask = group_ballot(act, lpe);
-  sc.inside = group_ballot(in, lpe) != 0;
+  sc.mask = 0;
+  sc.inside = false;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {
+    const bool has = lane + j * lpe < K;
+    const double rx = my[j].x - x, ry = my[j].y - y;
+    const double rr = rx * rx + ry * ry;
+    const bool in = has && (rr <= my[j].r * my[j].r);
+    const bool act = has && (in || !(sqrt(rr) - my[j].r > reach));
+    sc.mask |= group_ballot(act, lpe) << (j * lpe);
+    sc.inside = sc.inside || group_ballot(in, lpe) != 0;
+  }
   const double W = cfg.world_half;
   sc.wxp = (W - x) <= reach;
   sc.wxn = (x + W) <= reach;
@@ -451,9 +459,9 @@ FFMP_DEV float funkey(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (
 //    rounded minimum lidar_beam returns, and `h <= lidar_max` is decided in float64 per hit as there;
 //    h is never -0 (x - x = +0), so the minimum is the same value whatever order the hits arrive in.
 // Relies on the beam layout of ffmp_cfg_t.beam_cs (angle -pi + l 2pi/L).  lane / lpe: the env's
-// group; s_key: the env's L uint32 (LDS), s_pref / s_lo: its lpe ints each (LDS).  Every lane of
-// the group calls it (shuffles).  f(l, range) for every beam l.
-template <class F>
+// group, holding discs k = lane + j lpe (j < DPL); s_key: the env's L uint32 (LDS), s_pref / s_lo: its
+// lpe DPL ints each (LDS).  Every lane of the group calls it (shuffles).  f(l, range) for every beam l.
+template <int DPL, class F>
 FFMP_DEV void trace_discs(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane, int lpe, double x, double y,
                           double c, double s, const double* rxa, const double* rya, const double* rra,
                           const double* r2a, uint32_t* s_key, int* s_pref, int* s_lo, F&& f) {
@@ -466,39 +474,45 @@ FFMP_DEV void trace_discs(const ffmp_cfg_t& cfg, const LidarScene& sc, int lane,
   }
   const double W = cfg.world_half, L = cfg.lidar_max;
   for (int l = lane; l < nb; l += lpe) s_key[l] = fkey(__builtin_inff());
-  // this lane's disc: its beams [lo, lo + cnt) (mod L)
-  int lo = 0, cnt = 0;
-  if ((sc.mask >> lane) & 1ull) {
-    const double rx = rxa[lane], ry = rya[lane];
-    const float q = (float)(r2a[lane] / rra[lane]);  // sin^2 of the half-width
-    if (!(q < 0.98f)) {
-      cnt = nb;
-    } else {
-      const float ex = (float)(c * rx + s * ry), ey = (float)(c * ry - s * rx);  // the centre, robot frame
-      const float th = atan2f(ey, ex);
-      const float half = asinf(sqrtf(q)) + 1e-3f;
-      const float per = (float)nb * 0.159154943f;  // beams per radian
-      lo = (int)floorf((th - half + 3.14159265f) * per) - 1;
-      const int hi = (int)ceilf((th + half + 3.14159265f) * per) + 1;
-      cnt = min(hi - lo + 1, nb);
-      lo %= nb;
-      if (lo < 0) lo += nb;
+  // this lane's discs k = lane + j lpe: their beams [lo, lo + cnt) (mod L), and the inclusive
+  // prefix of the counts over the disc index k (pair p belongs to the first k with s_pref[k] > p)
+  int total = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {
+    const int k = lane + j * lpe;
+    int lo = 0, cnt = 0;
+    if ((sc.mask >> k) & 1ull) {
+      const double rx = rxa[k], ry = rya[k];
+      const float q = (float)(r2a[k] / rra[k]);  // sin^2 of the half-width
+      if (!(q < 0.98f)) {
+        cnt = nb;
+      } else {
+        const float ex = (float)(c * rx + s * ry), ey = (float)(c * ry - s * rx);  // the centre, robot frame
+        const float th = atan2f(ey, ex);
+        const float half = asinf(sqrtf(q)) + 1e-3f;
+        const float per = (float)nb * 0.159154943f;  // beams per radian
+        lo = (int)floorf((th - half + 3.14159265f) * per) - 1;
+        const int hi = (int)ceilf((th + half + 3.14159265f) * per) + 1;
+        cnt = min(hi - lo + 1, nb);
+        lo %= nb;
+        if (lo < 0) lo += nb;
+      }
     }
+    int incl = cnt;  // inclusive prefix over the group
+    for (int o = 1; o < lpe; o <<= 1) {
+      const int v = __shfl_up(incl, o, lpe);
+      if (lane >= o) incl += v;
+    }
+    s_pref[k] = total + incl;
+    s_lo[k] = lo;
+    total += __shfl(incl, lpe - 1, lpe);
   }
-  int incl = cnt;  // inclusive prefix over the group
-  for (int o = 1; o < lpe; o <<= 1) {
-    const int v = __shfl_up(incl, o, lpe);
-    if (lane >= o) incl += v;
-  }
-  const int total = __shfl(incl, lpe - 1, lpe);
-  s_pref[lane] = incl;
-  s_lo[lane] = lo;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   for (int p = lane; p < total; p += lpe) {
-    int k = 0;  // the disc of pair p: the first lane whose inclusive count exceeds p
-    for (int step = lpe >> 1; step > 0; step >>= 1)
+    int k = 0;  // the disc of pair p: the first disc whose inclusive count exceeds p
+    for (int step = (lpe * DPL) >> 1; step > 0; step >>= 1)
       if (s_pref[k + step - 1] <= p) k += step;
     int l = s_lo[k] + (p - (k ? s_pref[k - 1] : 0));
     if (l >= nb) l -= nb;

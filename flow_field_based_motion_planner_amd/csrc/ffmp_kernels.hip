@@ -112,7 +112,7 @@ Tuning& tuning() {
     if (const char* v = getenv("FFMP_RASTER_LDS_PAD")) r.lds_pad = std::max(0, std::min(atoi(v), 65536));
     if (const char* v = getenv("FFMP_ENV_LANES")) {
       const int l = atoi(v);
-      r.env_lanes = (l == 16 || l == 32 || l == 64) ? l : 0;
+      r.env_lanes = (l == 4 || l == 8 || l == 16 || l == 32 || l == 64) ? l : 0;
     }
     return r;
   }();
@@ -164,8 +164,7 @@ __device__ uint64_t g_trace_ras[65536 * 4];
 
 // One env's raster record: header, goal, then K float4 of each of cur / prev / vel.
 // Lane k writes obstacle k; lanes 0..3 the header words.
-FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const FrameHdr& hc, const FrameHdr& hp,
-                           float2 ge, float4 ecur, float4 eprev, float4 vel, float first) {
+FFMP_DEV void write_record_hdr(float* rec, int lane, const FrameHdr& hc, const FrameHdr& hp, float2 ge, float first) {
   if (lane == 0) {
     rec[8] = ge.x;
     rec[9] = ge.y;
@@ -177,12 +176,13 @@ FFMP_DEV void write_record(float* rec, int lane, int K, bool has_obst, const Fra
     rec[4 + lane] = lane == 0 ? hp.px : lane == 1 ? hp.py : lane == 2 ? hp.c : hp.s;
     rec[12 + lane] = 0.0f;
   }
-  if (has_obst) {
-    float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
-    ro[lane] = ecur;
-    ro[K + lane] = eprev;
-    ro[2 * K + lane] = vel;
-  }
+}
+// disc k of K: its current and previous ego disc and its ego velocity
+FFMP_DEV void write_record_obst(float* rec, int k, int K, float4 ecur, float4 eprev, float4 vel) {
+  float4* ro = reinterpret_cast<float4*>(rec + FFMP_REC_HDR);
+  ro[k] = ecur;
+  ro[K + k] = eprev;
+  ro[2 * K + k] = vel;
 }
 
 // The lidar beam table {cos, sin} (cfg.beam_cs, (L, 2) float64) is read one beam ahead: lane
@@ -246,7 +246,7 @@ FFMP_DEV void stage_footprint(const ffmp_cfg_t& cfg, float2* s_foot) {
 // cells are strided over the group's lanes.
 // One env's step (or reset) by its LPE-lane group: lane = the lane within the group, s_* = the
 // group's LDS slices (FFMP_MAX_OBST entries each).  Used by env_kernel and step_raster_kernel.
-template <int MODE, int LPE, int BCH = FFMP_BEAM_CHUNK, bool DL = false>
+template <int MODE, int LPE, int BCH = FFMP_BEAM_CHUNK, bool DL = false, int DPL = 1>
 FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, int64_t env_offset,
                                                        const int64_t* __restrict__ action, int32_t initial,
                                                        const ffmp_state_t& st, const ffmp_obs_t& ob,
@@ -255,7 +255,8 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
                                                        float4* s_eprev, const float2* s_foot, float* s_rhdr = nullptr,
                                                        float2* s_rvel = nullptr, uint32_t* s_key = nullptr,
                                                        int* s_pref = nullptr, int* s_lo = nullptr) {
-  static_assert(LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
+  static_assert(LPE == 4 || LPE == 8 || LPE == 16 || LPE == 32 || LPE == 64, "lanes per env");
+  static_assert(DPL == 1 || DPL == 2 || DPL == 4, "discs per lane");
   const int K = cfg.n_obst;
   const int L = cfg.n_beams;
   const int G = cfg.grid;
@@ -264,18 +265,24 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
   FFMP_ENV_STAMP(0);
   const double2 beam0 = first_beam(cfg, lane);  // in flight during the integrator's chain
 
-  // ---- load (uniform scalars in every lane; obstacle k in lane k) ----
+  // ---- load (uniform scalars in every lane; discs k = lane + j LPE, j < DPL, in this lane) ----
   double x0 = st.pose[e * 3 + 0], y0 = st.pose[e * 3 + 1], yaw0 = st.pose[e * 3 + 2];
   double gx = st.goal[e * 2 + 0], gy = st.goal[e * 2 + 1];
   double d0 = st.d0[e];
   int32_t t = st.t[e];
   int32_t episode = st.episode[e];
-  Obst my{0.0, 0.0, 0.0, 0.0, 0.0};
-  const bool has_obst = lane < K;
-  if (MODE == kEnvMode_Step && has_obst) {
-    const double* p = st.obst + (e * K + lane) * 4;
-    my.x = p[0]; my.y = p[1]; my.vx = p[2]; my.vy = p[3];
-    my.r = st.obst_r[e * K + lane];
+  Obst my[DPL];
+  bool has_obst[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {
+    const int k = lane + j * LPE;
+    has_obst[j] = k < K;
+    my[j] = Obst{0.0, 0.0, 0.0, 0.0, 0.0};
+    if (MODE == kEnvMode_Step && has_obst[j]) {
+      const double* p = st.obst + (e * K + k) * 4;
+      my[j].x = p[0]; my[j].y = p[1]; my[j].vx = p[2]; my[j].vy = p[3];
+      my[j].r = st.obst_r[e * K + k];
+    }
   }
 
   double x1 = x0, y1 = y0, yaw1 = yaw0;
@@ -299,10 +306,12 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     y1 = y0 + (v * s0) * cfg.dt;
     yaw1 = pi_to_pi(yaw0 + w * cfg.dt);
     // previous frame record from the pre-step pose / obstacle positions
-    if (has_obst) {
-      s_eprev[lane] = ego_obst(my, x0, y0, c0, s0);
-      if (cfg.moving) move_obstacle(cfg, my);
-    }
+#pragma unroll
+    for (int j = 0; j < DPL; ++j)
+      if (has_obst[j]) {
+        s_eprev[lane + j * LPE] = ego_obst(my[j], x0, y0, c0, s0);
+        if (cfg.moving) move_obstacle(cfg, my[j]);
+      }
     t = t + 1;
     // ---- velocity (train.py:182-188): per-step displacement ----
     const double ddx = x1 - x0, ddy = y1 - y0;
@@ -312,10 +321,16 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
   }
   FFMP_ENV_STAMP(1);
 
-  if (has_obst) lidar_disc(x1, y1, my.x, my.y, my.r, s_ox, s_oy, s_orr, s_or, lane);
+#pragma unroll
+  for (int j = 0; j < DPL; ++j)
+    if (has_obst[j]) lidar_disc(x1, y1, my[j].x, my[j].y, my[j].r, s_ox, s_oy, s_orr, s_or, lane + j * LPE);
   double c1 = cos(yaw1), s1 = sin(yaw1);
-  const float4 ecur1 = has_obst ? ego_obst(my, x1, y1, c1, s1) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (has_obst) s_ecur[lane] = ecur1;
+  float4 ecur1[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {
+    ecur1[j] = has_obst[j] ? ego_obst(my[j], x1, y1, c1, s1) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (has_obst[j]) s_ecur[lane + j * LPE] = ecur1[j];
+  }
   wave_sync();
 
   FFMP_ENV_STAMP(2);
@@ -342,27 +357,31 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       ob.grad[e * 2 + 0] = (Uxp - Uxm) * cfg.inv_2res_f;
       ob.grad[e * 2 + 1] = (Uyp - Uym) * cfg.inv_2res_f;
     }
-    const float4 ecur = has_obst ? s_ecur[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 eprev = has_obst ? s_eprev[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 vel = ego_vel(my, c1, s1);
-    write_record(st.record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel,
-                 first ? 1.0f : 0.0f);
-    if (s_rhdr) {  // the one-launch step: the record's header (and velocities) for the block's raster, in LDS
+    float* rec = st.record + e * rec_stride(K);
+    // the terminal state (keep_terminal): the post-step record of a stepped env — also when it
+    // resets below, which rewrites only st.record
+    float* term = (MODE == kEnvMode_Step && !first && st.term_record) ? st.term_record + e * rec_stride(K) : nullptr;
+    write_record_hdr(rec, lane, hcur, hprev, ge, first ? 1.0f : 0.0f);
+    if (term) write_record_hdr(term, lane, hcur, hprev, ge, 0.0f);
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) {
+      if (!has_obst[j]) continue;
+      const int k = lane + j * LPE;
+      const float4 ecur = s_ecur[k], eprev = s_eprev[k];
+      const float4 vel = ego_vel(my[j], c1, s1);
+      write_record_obst(rec, k, K, ecur, eprev, vel);
+      if (term) write_record_obst(term, k, K, ecur, eprev, vel);
+      if (s_rvel) s_rvel[k] = make_float2(vel.x, vel.y);
+      double* p = st.obst + (e * K + k) * 4;
+      p[0] = my[j].x; p[1] = my[j].y; p[2] = my[j].vx; p[3] = my[j].vy;
+      st.obst_r[e * K + k] = my[j].r;
+    }
+    if (s_rhdr) {  // the one-launch step: the record's header for the block's raster, in LDS
       if (lane < FFMP_REC_HDR) {
         const float hv[FFMP_REC_HDR] = {hcur.px, hcur.py, hcur.c, hcur.s, hprev.px, hprev.py, hprev.c, hprev.s,
                                         ge.x,    ge.y,    first ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         s_rhdr[lane] = hv[lane];
       }
-      if (s_rvel && has_obst) s_rvel[lane] = make_float2(vel.x, vel.y);
-    }
-    // the terminal state (keep_terminal): the post-step record of a stepped env — also when it
-    // resets below, which rewrites only st.record
-    if (MODE == kEnvMode_Step && !first && st.term_record)
-      write_record(st.term_record + e * rec_stride(K), lane, K, has_obst, hcur, hprev, ge, ecur, eprev, vel, 0.0f);
-    if (has_obst) {
-      double* p = st.obst + (e * K + lane) * 4;
-      p[0] = my.x; p[1] = my.y; p[2] = my.vx; p[3] = my.vy;
-      st.obst_r[e * K + lane] = my.r;
     }
     if (lane == 0) {
       st.pose[e * 3 + 0] = x1; st.pose[e * 3 + 1] = y1; st.pose[e * 3 + 2] = yaw1;
@@ -406,22 +425,30 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       const float2 fb = s_foot[FFMP_MAX_FOOT];
       const float Wf = cfg.world_half_f * 0.9999f, reach = (fb.x + fb.y) * 1.0001f + 1e-6f;
       const bool wall = !(fabsf(hcur.px) + reach < Wf && fabsf(hcur.py) + reach < Wf);
-      const float rr = ecur1.w * 1.0001f + 1e-6f;
-      const bool disc = has_obst && !(fabsf(ecur1.x) - fb.x > rr || fabsf(ecur1.y) - fb.y > rr);
-      if (__ballot(disc || (wall && lane == 0)) != 0) {
+      bool disc[DPL], anyd = false;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) {
+        const float rr = ecur1[j].w * 1.0001f + 1e-6f;
+        disc[j] = has_obst[j] && !(fabsf(ecur1[j].x) - fb.x > rr || fabsf(ecur1[j].y) - fb.y > rr);
+        anyd = anyd || disc[j];
+      }
+      if (__ballot(anyd || (wall && lane == 0)) != 0) {
         for (int f = 0; f < cfg.n_foot; ++f) {
           const float2 fc = s_foot[f];
           const float ex = fc.x, ey = fc.y;
-          c_foot |= (disc && in_disc(ex, ey, ecur1)) || (wall && lane == 0 && outside_world(cfg, hcur, ex, ey));
+          bool hit = wall && lane == 0 && outside_world(cfg, hcur, ex, ey);
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) hit = hit || (disc[j] && in_disc(ex, ey, ecur1[j]));
+          c_foot |= hit;
         }
       }
     }
     FFMP_ENV_STAMP(7);
     // ---- lidar + is_collision2 (ffmp.py:108-117) ----
     bool c_lidar = false;
-    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
+    const LidarScene sc = lidar_scene<DPL>(cfg, x1, y1, my, lane, K, LPE);
     if constexpr (DL) {
-      trace_discs(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo, [&](int l, double r) {
+      trace_discs<DPL>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo, [&](int l, double r) {
         const float rf = (float)r;
         ob.lidar[e * L + l] = rf;
         c_lidar |= beam_collides(rf, cfg.robot_r);
@@ -466,14 +493,19 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
     const Episode ep = sample_episode(cfg, genv, episode);
     x1 = ep.x; y1 = ep.y; yaw1 = ep.yaw; gx = ep.gx; gy = ep.gy;
     wave_sync();  // all lanes done reading the terminal-state LDS arrays
-    if (has_obst) my = sample_obstacle(cfg, genv, episode, lane, ep);
+#pragma unroll
+    for (int j = 0; j < DPL; ++j)
+      if (has_obst[j]) my[j] = sample_obstacle(cfg, genv, episode, lane + j * LPE, ep);
     c1 = cos(yaw1); s1 = sin(yaw1);
-    if (has_obst) {
-      lidar_disc(x1, y1, my.x, my.y, my.r, s_ox, s_oy, s_orr, s_or, lane);
-      const float4 eo = ego_obst(my, x1, y1, c1, s1);
-      s_ecur[lane] = eo;
-      s_eprev[lane] = eo;  // temporal stack duplicated on the first step (train.py:475-478)
-    }
+#pragma unroll
+    for (int j = 0; j < DPL; ++j)
+      if (has_obst[j]) {
+        const int k = lane + j * LPE;
+        lidar_disc(x1, y1, my[j].x, my[j].y, my[j].r, s_ox, s_oy, s_orr, s_or, k);
+        const float4 eo = ego_obst(my[j], x1, y1, c1, s1);
+        s_ecur[k] = eo;
+        s_eprev[k] = eo;  // temporal stack duplicated on the first step (train.py:475-478)
+      }
     wave_sync();
     hcur = make_hdr(x1, y1, c1, s1);
     hprev = hcur;
@@ -487,9 +519,9 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
       ob.state_g[e * 2 + 0] = (float)dist;
       ob.state_g[e * 2 + 1] = (float)pi_to_pi(atan2(dy, dx) - yaw1);
     }
-    const LidarScene sc = lidar_scene(cfg, x1, y1, my.x, my.y, my.r, has_obst, LPE);
+    const LidarScene sc = lidar_scene<DPL>(cfg, x1, y1, my, lane, K, LPE);
     if constexpr (DL) {
-      trace_discs(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo,
+      trace_discs<DPL>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or, s_key, s_pref, s_lo,
                   [&](int l, double r) { ob.lidar[e * L + l] = (float)r; });
     } else if constexpr (BCH > 1) {
       trace_beams<BCH>(cfg, sc, lane, LPE, x1, y1, c1, s1, s_ox, s_oy, s_orr, s_or,
@@ -510,20 +542,20 @@ FFMP_DEV __attribute__((always_inline)) void env_group(const ffmp_cfg_t& cfg, in
 #else
 #define FFMP_ENV_OCC
 #endif
-template <int MODE, int kEnvWaves, int LPE>
+template <int MODE, int kEnvWaves, int LPE, int DPL>
 __global__ __launch_bounds__(64 * kEnvWaves) FFMP_ENV_OCC void env_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
                                                  const int64_t* __restrict__ action,
                                                  const uint8_t* __restrict__ mask, int32_t initial,
                                                  ffmp_state_t st, ffmp_obs_t ob, ffmp_out_t out) {
   constexpr int EPW = 64 / LPE;  // envs per wave
-  __shared__ double s_oxa[kEnvWaves][FFMP_MAX_OBST], s_oya[kEnvWaves][FFMP_MAX_OBST],
-      s_ora[kEnvWaves][FFMP_MAX_OBST], s_orra[kEnvWaves][FFMP_MAX_OBST];
-  __shared__ float4 s_ecura[kEnvWaves][FFMP_MAX_OBST], s_epreva[kEnvWaves][FFMP_MAX_OBST];
+  constexpr int DS = 64 * DPL;    // disc slots per wave: EPW envs x LPE lanes x DPL discs
+  __shared__ double s_oxa[kEnvWaves][DS], s_oya[kEnvWaves][DS], s_ora[kEnvWaves][DS], s_orra[kEnvWaves][DS];
+  __shared__ float4 s_ecura[kEnvWaves][DS], s_epreva[kEnvWaves][DS];
   __shared__ float2 s_foota[kEnvWaves][FFMP_MAX_FOOT + 1];  // + the cells' extent
   // the disc-major lidar's per-env beam minima ([wave][env][L] uint32, dynamic: L * 4 bytes per env)
   // and per-disc pair counts / first beams
   extern __shared__ uint32_t s_keys[];
-  __shared__ int s_prefa[kEnvWaves][64], s_loa[kEnvWaves][64];
+  __shared__ int s_prefa[kEnvWaves][DS], s_loa[kEnvWaves][DS];
 
   const int wv = threadIdx.x >> 6;
   const int grp = (threadIdx.x & 63) / LPE;
@@ -532,11 +564,11 @@ __global__ __launch_bounds__(64 * kEnvWaves) FFMP_ENV_OCC void env_kernel(ffmp_c
   if (MODE == kEnvMode_Step) stage_footprint(cfg, s_foota[wv]);
   if (e >= n) return;
   if (MODE == kEnvMode_Reset && mask && !mask[e]) return;
-  env_group<MODE, LPE, FFMP_BEAM_CHUNK, true>(cfg, env_offset, action, initial, st, ob, out, e, lane,
-                       s_oxa[wv] + grp * LPE, s_oya[wv] + grp * LPE, s_ora[wv] + grp * LPE, s_orra[wv] + grp * LPE,
-                       s_ecura[wv] + grp * LPE, s_epreva[wv] + grp * LPE, s_foota[wv], nullptr, nullptr,
-                       s_keys + ((size_t)wv * EPW + grp) * cfg.n_beams, s_prefa[wv] + grp * LPE,
-                       s_loa[wv] + grp * LPE);
+  const int g0 = grp * LPE * DPL;  // the env's disc slots
+  env_group<MODE, LPE, FFMP_BEAM_CHUNK, true, DPL>(cfg, env_offset, action, initial, st, ob, out, e, lane,
+                       s_oxa[wv] + g0, s_oya[wv] + g0, s_ora[wv] + g0, s_orra[wv] + g0,
+                       s_ecura[wv] + g0, s_epreva[wv] + g0, s_foota[wv], nullptr, nullptr,
+                       s_keys + ((size_t)wv * EPW + grp) * cfg.n_beams, s_prefa[wv] + g0, s_loa[wv] + g0);
 }
 
 // ============================================================================
@@ -1314,30 +1346,40 @@ static int check_episode(const ffmp_episode_t* ep) {
   return FFMP_OK;
 }
 
-template <int MODE, int W, int LPE>
+template <int MODE, int W, int LPE, int DPL>
 void launch_env_t(const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action, const uint8_t* mask,
                   int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob, const ffmp_out_t& o,
                   hipStream_t s) {
   const int64_t per_block = (int64_t)W * (64 / LPE);
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const size_t lds = (size_t)W * (64 / LPE) * (size_t)cfg.n_beams * sizeof(uint32_t);  // trace_discs' beam minima
-  hipLaunchKernelGGL((env_kernel<MODE, W, LPE>), dim3(blocks), dim3(64 * W), lds, s, cfg, n, env_offset, action, mask,
-                     initial, st, ob, o);
+  hipLaunchKernelGGL((env_kernel<MODE, W, LPE, DPL>), dim3(blocks), dim3(64 * W), lds, s, cfg, n, env_offset, action,
+                     mask, initial, st, ob, o);
+}
+
+// (lanes per env, discs per lane) pairs with an env_kernel instance; false if there is none
+template <int MODE, int W>
+bool launch_env_mode(int lpe, int dpl, const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action,
+                     const uint8_t* mask, int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob,
+                     const ffmp_out_t& o, hipStream_t s) {
+#define FFMP_ENV_CASE(L_, D_)                                                                    \
+  if (lpe == L_ && dpl == D_) {                                                                  \
+    launch_env_t<MODE, W, L_, D_>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);      \
+    return true;                                                                                 \
+  }
+  FFMP_ENV_CASE(16, 1) FFMP_ENV_CASE(32, 1) FFMP_ENV_CASE(64, 1) FFMP_ENV_CASE(8, 2) FFMP_ENV_CASE(16, 2)
+  FFMP_ENV_CASE(4, 4) FFMP_ENV_CASE(8, 1)
+#undef FFMP_ENV_CASE
+  return false;
 }
 
 template <int W>
-void launch_env_lpe(int mode, int lpe, const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action,
-                    const uint8_t* mask, int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob,
-                    const ffmp_out_t& o, hipStream_t s) {
-  if (mode == kEnvMode_Step) {
-    if (lpe == 16) launch_env_t<kEnvMode_Step, W, 16>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-    else if (lpe == 32) launch_env_t<kEnvMode_Step, W, 32>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-    else launch_env_t<kEnvMode_Step, W, 64>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-  } else {
-    if (lpe == 16) launch_env_t<kEnvMode_Reset, W, 16>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-    else if (lpe == 32) launch_env_t<kEnvMode_Reset, W, 32>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-    else launch_env_t<kEnvMode_Reset, W, 64>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
-  }
+bool launch_env_lpe(int mode, int lpe, int dpl, const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset,
+                    const int64_t* action, const uint8_t* mask, int32_t initial, const ffmp_state_t& st,
+                    const ffmp_obs_t& ob, const ffmp_out_t& o, hipStream_t s) {
+  if (mode == kEnvMode_Step)
+    return launch_env_mode<kEnvMode_Step, W>(lpe, dpl, cfg, n, env_offset, action, mask, initial, st, ob, o, s);
+  return launch_env_mode<kEnvMode_Reset, W>(lpe, dpl, cfg, n, env_offset, action, mask, initial, st, ob, o, s);
 }
 
 // ============================================================================
@@ -1455,8 +1497,8 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       t.env_waves = value;
       return prev;
     case FFMP_TUNE_ENV_LANES:
-      if (value != 0 && value != 16 && value != 32 && value != 64)
-        return fail(FFMP_E_ARG, "env lanes must be 0 (auto), 16, 32 or 64");
+      if (value != 0 && value != 4 && value != 8 && value != 16 && value != 32 && value != 64)
+        return fail(FFMP_E_ARG, "env lanes must be 0 (auto), 4, 8, 16, 32 or 64");
       prev = t.env_lanes;
       t.env_lanes = value;
       return prev;
@@ -1536,13 +1578,26 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
   // the per-env scalar work dominates and fewer, longer beam loops win: C3 (K = 16, L = 180) 79 us
   // at 32 lanes -> 68 at 16, the C5 share (K = 32, L = 360) 83 at 64 -> 77 at 32
   // (profiles/r03c_beam_chunk.txt).
-  const int need = cfg->n_obst <= 16 ? 16 : cfg->n_obst <= 32 ? 32 : 64;
-  const int autol = need;
-  const int lpe = tu.env_lanes ? (tu.env_lanes >= need ? tu.env_lanes : need) : autol;
-  if (tu.env_waves == 4)
-    launch_env_lpe<4>(mode, lpe, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, (hipStream_t)stream);
-  else
-    launch_env_lpe<1>(mode, lpe, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, (hipStream_t)stream);
+  // Round 4: a lane may hold several discs (k = lane + j * lanes, j < discs per lane), so that more
+  // envs share a wave: FFMP_TUNE_ENV_LANES picks the lanes per env and the discs per lane follow
+  // (ceil(K / lanes)); a pair without a kernel instance falls back to one disc per lane.  Measured
+  // (profiles/r04k_env_lanes.txt): two discs per lane at 8 lanes is slower at C3 (52.5 vs 43.7 us:
+  // the lidar's (disc, beam) pairs are shared by half the lanes; the rest takes the same 30 us), so
+  // the default stays one disc per lane, the fewest lanes that hold them — 8 for K <= 8 (C2 12.1 vs
+  // 12.6 us at 16).
+  const int need = cfg->n_obst <= 8 ? 8 : cfg->n_obst <= 16 ? 16 : cfg->n_obst <= 32 ? 32 : 64;
+  int lpe = tu.env_lanes ? tu.env_lanes : need;
+  int dpl = cfg->n_obst <= lpe ? 1 : (cfg->n_obst + lpe - 1) / lpe;
+  const hipStream_t hs = (hipStream_t)stream;
+  const bool w4 = tu.env_waves == 4;
+  bool ok = w4 ? launch_env_lpe<4>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs)
+               : launch_env_lpe<1>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs);
+  if (!ok) {
+    lpe = need;
+    dpl = 1;
+    ok = w4 ? launch_env_lpe<4>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs)
+            : launch_env_lpe<1>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs);
+  }
   return check_launch(mode == kEnvMode_Step ? "ffmp_step_state" : "ffmp_reset");
 }
 

@@ -182,7 +182,7 @@ int64_t ffmp_layout(int32_t which);
 #define FFMP_TUNE_RASTER_NT 2   /* raster stores: 0 by plane size, 1 plain, 2 nontemporal  */
 #define FFMP_TUNE_RASTER_XCD 3  /* 1: XCD-aware block remap                                */
 #define FFMP_TUNE_ENV_WAVES 4   /* waves per env_kernel block: 1 or 4                       */
-#define FFMP_TUNE_ENV_LANES 5   /* lanes per env in env_kernel: 0 auto, 16, 32, 64 (>= K)   */
+#define FFMP_TUNE_ENV_LANES 5   /* lanes per env in env_kernel: 0 auto, 4, 8, 16, 32, 64 (a lane holds ceil(K / lanes) discs) */
 #define FFMP_TUNE_RING_EXTRA 6  /* ffmp_ring_create / rebuild: fresh pieces allocated beyond the
                                    ones the ring needs (pairing candidates; they stay pooled):
                                    0 = default (need/2 + 4), v >= 1 = at most v - 1.  An HBM

@@ -427,15 +427,17 @@ def test_no_potential_same_frames():
             assert "potential" not in ob
 
 
-def test_env_lanes_identical():
-    """Every lanes-per-env layout of env_kernel (1, 2 or 4 envs per wave) gives the same state,
-    observations and flags, bit for bit, through resets (and matches the oracle)."""
+@pytest.mark.parametrize("K,lanes_list", [(12, (16, 32, 64)), (16, (4, 8, 16, 32, 64)), (24, (16, 8, 32, 64))])
+def test_env_lanes_identical(K, lanes_list):
+    """Every lanes-per-env layout of env_kernel — 1, 2, 4 envs per wave with one disc per lane, and
+    (round 4) 8 or 16 envs per wave with 2 or 4 discs per lane — gives the same state, observations
+    and flags, bit for bit, through resets (and matches the oracle)."""
     from flow_field_based_motion_planner_amd import _abi
-    cfg = FFMPConfig(grid=64, n_obst=12, n_beams=40, moving=True, obst_rmax=0.5, obst_vmax=1.2, world_half=2.6,
+    cfg = FFMPConfig(grid=64, n_obst=K, n_beams=40, moving=True, obst_rmax=0.5, obst_vmax=1.2, world_half=2.6,
                      max_steps=5, seed=44)
     snaps = {}
     try:
-        for lanes in (16, 32, 64):
+        for lanes in lanes_list:
             _abi.set_tuning(_abi.TUNE_ENV_LANES, lanes)
             env, ref, problems, counts = _run(cfg, 23, 10, frame_window=3)
             assert not problems, (lanes, problems[:5])
@@ -443,7 +445,8 @@ def test_env_lanes_identical():
             snaps[lanes] = gpu_snapshot(env)
     finally:
         _abi.set_tuning(_abi.TUNE_ENV_LANES, 0)
-    for k in snaps[16]:
-        if snaps[16][k] is not None:
-            assert np.array_equal(snaps[16][k], snaps[32][k], equal_nan=True), k
-            assert np.array_equal(snaps[16][k], snaps[64][k], equal_nan=True), k
+    first = snaps[lanes_list[0]]
+    for lanes in lanes_list[1:]:
+        for k in first:
+            if first[k] is not None:
+                assert np.array_equal(first[k], snaps[lanes][k], equal_nan=True), (lanes, k)

@@ -489,8 +489,11 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
   FFMP_WGRAD_STORE1(4) FFMP_WGRAD_STORE1(5) FFMP_WGRAD_STORE1(6) FFMP_WGRAD_STORE1(7)              \
   FFMP_WGRAD_STORE1(8) FFMP_WGRAD_STORE1(9) FFMP_WGRAD_STORE1(10) FFMP_WGRAD_STORE1(11)
 
+#ifndef FFMP_WGRAD_TW_3264
+#define FFMP_WGRAD_TW_3264 4  // taps per wave of the 32 -> 64 weight gradient (probe knob)
+#endif
 template <int C, int N, int TW>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
+__global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
                                                             float* __restrict__ part, int B, int H, int W, int KH,
                                                             int KW, int dx, int TKY, int TKX, int R, int per_chunk) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -693,7 +696,7 @@ int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t ba
                 batch, h, wd, kh, kw, dx, chunks);
   if (((uintptr_t)g | (uintptr_t)x) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: g and x must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  if (c == 32 && n == 64) return launch_wgrad<32, 64, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  if (c == 32 && n == 64) return launch_wgrad<32, 64, FFMP_WGRAD_TW_3264>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 64 && n == 64) return launch_wgrad<64, 64, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 32 && n == 32) return launch_wgrad<32, 32, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 64 && n == 32) return launch_wgrad<64, 32, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);

@@ -111,8 +111,8 @@ def conv2d_wgrad_nhwc(g: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dx: in
     Bg, Ho, Wo, N = g.shape
     if Bg != B or Ho != H - KH + 1 or Wo != W - (KW - 1) * dx:
         raise ValueError(f"shape mismatch: g {tuple(g.shape)}, x {tuple(x.shape)}, kernel {KH}x{KW} dx {dx}")
-    if chunks is None:  # ~512 workgroups (taps per workgroup: 16 at 32 -> 64 channels, else 8)
-        groups = KH * KW // (16 if (Cin, N) == (32, 64) else 8)
+    if chunks is None:  # ~512 workgroups (taps per workgroup: 32 at 32 -> 64 channels, else 8)
+        groups = KH * KW // (32 if (Cin, N) == (32, 64) else 8)
         chunks = max(1, min(B, 512 // max(groups, 1)))
     part = torch.empty((chunks, KH, KW, N, Cin), dtype=torch.float32, device=g.device)
     stream = C.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)

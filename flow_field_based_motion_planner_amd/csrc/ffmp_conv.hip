@@ -489,8 +489,11 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
   FFMP_WGRAD_STORE1(4) FFMP_WGRAD_STORE1(5) FFMP_WGRAD_STORE1(6) FFMP_WGRAD_STORE1(7)              \
   FFMP_WGRAD_STORE1(8) FFMP_WGRAD_STORE1(9) FFMP_WGRAD_STORE1(10) FFMP_WGRAD_STORE1(11)
 
+// taps per wave of the 32 -> 64 weight gradient (conv2's): 8 (256 accumulators, one wave per SIMD)
+// re-reads the stage images for half as many tap groups as 4: 1.73 vs 1.82-1.88 ms at B = 256
+// (profiles/r04l_wgrad.txt)
 #ifndef FFMP_WGRAD_TW_3264
-#define FFMP_WGRAD_TW_3264 4  // taps per wave of the 32 -> 64 weight gradient (probe knob)
+#define FFMP_WGRAD_TW_3264 8
 #endif
 template <int C, int N, int TW>
 __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,

@@ -615,7 +615,14 @@ class FFMPVec:
             # the tuning launches (and _clear_after_tuning's memsets) must be done before the
             # rebuild's pairing probes write the potential plane on their own stream
             torch.cuda.synchronize(self.device)
-            self._ring.rebuild(sum(1 << i for i in slow), partner=self.potential, keep_old=True)
+            try:
+                self._ring.rebuild(sum(1 << i for i in slow), partner=self.potential, keep_old=True)
+            except _abi.FFMPBackendError as err:
+                # the rebuild maps the new pieces beside the old ring: with the HBM shared (several
+                # ranks on one device) it can run out; the current ring is whole and stays, and the
+                # pieces the rebuild took went back to the pool (trimmed below / in __init__)
+                history.append({"skipped": str(err)[:200]})
+                break
             self._adopt_ring_tensor()
             new = self._slot_ms()
             if sum(new.values()) < sum(ms.values()):

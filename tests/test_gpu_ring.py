@@ -156,6 +156,35 @@ def test_repair_keeps_a_working_ring():
         assert torch.equal(oa["state_m"], ob["state_m"]) and torch.equal(oa["potential"], ob["potential"])
 
 
+def test_repair_survives_a_failed_rebuild():
+    """A slot rebuild that fails (out of HBM with several ranks on one device: bench.py --gpus 4
+    rehearsed on one GPU, profiles/r04n_launcher.txt) leaves the current ring in place; the repair
+    records the reason and the env still matches the contiguous layout bit for bit."""
+    from flow_field_based_motion_planner_amd import _abi
+    from flow_field_based_motion_planner_amd.config import FFMPConfig
+    from flow_field_based_motion_planner_amd.vec_env import FFMPVec
+    cfg = FFMPConfig(grid=64, n_obst=6, n_beams=16, moving=True, max_steps=6, seed=9)
+    a = FFMPVec(12, cfg, device="cuda:0", frame_window=2)
+    b = FFMPVec(12, cfg, device="cuda:0", frame_window=4, seamless=True, autotune=False)
+    handle = b._ring.handle
+
+    def no_memory(*args, **kw):
+        raise _abi.FFMPBackendError("ffmp_ring_rebuild failed (rc=-2): out of memory (test)")
+
+    b._ring.rebuild = no_memory
+    b.SLOW_SLOT = -1.0
+    b._repair_slots()
+    assert b._ring.handle == handle and b._ring.info()["rebuilds"] == 0
+    assert "out of memory" in b.ring_meta["repair"][-1]["skipped"]
+    a.reset()
+    b.reset()
+    g = torch.Generator().manual_seed(2)
+    for _ in range(10):
+        act = torch.randint(0, 28, (12,), generator=g).to("cuda:0")
+        oa, ob = a.step(act)[0], b.step(act)[0]
+        assert torch.equal(oa["state_m"], ob["state_m"]) and torch.equal(oa["potential"], ob["potential"])
+
+
 def test_partner_relocation_keeps_a_consistent_env():
     """With every pairing probe declared slow, FFMPVec re-allocates the potential plane's arena and
     re-pairs a ring against it (up to PARTNER_TRIES times), keeping the best pair; the kept arena

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 OBS_F32, OBS_U8F16 = 0, 1  # include/ffmp.h FFMP_OBS_*
 MAX_SERIES = 16  # FFMP_MAX_SERIES (ffmp_temporal_maps)
 
@@ -121,6 +121,7 @@ _SIGS = {
     "ffmp_episode_update": (C.c_int, [_I64, C.POINTER(OutT), _I32, _I32, C.c_double, _I32, C.POINTER(EpisodeT),
                                       _P]),
     "ffmp_temporal_maps": (C.c_int, [_I64, _P, C.POINTER(_I64), _I32, _I64, _I64, _I32, _P, _P, _P]),
+    "ffmp_bev_image": (C.c_int, [_I64, _I32, _P, _I64, _P, _I64, C.c_float, _P, _I64, _P]),
     "ffmp_ring_create": (C.c_int, [_I32, _I64, _I32, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "ffmp_ring_info": (C.c_int, [_P, C.POINTER(C.c_double), _I32]),
     "ffmp_ring_rebuild": (C.c_int, [_P, C.c_uint64, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),

@@ -166,18 +166,25 @@ def conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 #   y[b, yo, xo, n] = sum_{ky, kx', q} x'[b, yo+ky, xo+kx'*F, q] w'[ky, kx', n, q]
 # the same products and sum as the original, on the MFMA kernel.
 
+def fold_channels(c: int) -> int:
+    """The channels a c-channel input is zero-padded to before folding: the next power of two
+    (3 -> 4, 12 -> 16), so F = 32 / that kernel columns fill the 32 folded channels."""
+    return 1 << (int(c) - 1).bit_length()
+
+
 def fold_supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
-    """A 1-4 channel layer whose kernel width folds into 32 channels; with the input's NCHW shape,
-    also the folded forward and weight-gradient launches (the input gradient is MIOpen's)."""
+    """A 1-16 channel layer whose kernel width folds into 32 channels (padded to a power of two:
+    the reference's 1 / 2 / 3 map channels and the 12-channel BEV series); with the input's NCHW
+    shape, also the folded forward and weight-gradient launches (the input gradient is MIOpen's)."""
     c = conv.in_channels
-    if not (_layer_ok(conv) and c in (1, 2, 3, 4) and conv.kernel_size[1] % (32 // (4 if c == 3 else c)) == 0
+    if not (_layer_ok(conv) and 1 <= c <= 16 and conv.kernel_size[1] % (32 // fold_channels(c)) == 0
             and conv.out_channels in (32, 64)):
         return False
     if x_shape is None:
         return True
     B, Cx, H, W = (int(v) for v in x_shape)
     KH, KW = conv.kernel_size
-    F = 32 // (4 if c == 3 else c)
+    F = 32 // fold_channels(c)
     if Cx != c or H < KH or W < KW:
         return False
     return (shape_ok(0, B, H, W - F + 1, 32, KH, KW // F, conv.out_channels, 0, F)
@@ -201,7 +208,7 @@ def pack_weight_fold(w: torch.Tensor, F: int) -> torch.Tensor:
 
 
 class MFMAFoldConv2dReLU(torch.autograd.Function):
-    """relu(conv2d(x, weight, bias)) for a 1/2/4-channel x on the MFMA kernel (kernel columns folded
+    """relu(conv2d(x, weight, bias)) for a 1/2/4/8/16-channel x on the MFMA kernel (kernel columns folded
     into 32 channels); bf16 NCHW-shaped result (channels-last strides).  Backward: the weight
     gradient of the folded convolution on the MFMA kernel, unfolded; the input's (MIOpen) only if
     asked for."""
@@ -239,7 +246,8 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
 def fold_conv_relu(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """relu(conv(x)) for a few-channel conv (the reference's conv1) through the MFMA kernel."""
     w = conv.weight
-    if x.shape[1] == 3:  # a zero 4th channel (zero products) keeps the fold at F = 8 columns
-        x = torch.nn.functional.pad(x, (0, 0, 0, 0, 0, 1))
-        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 1))
+    pad = fold_channels(x.shape[1]) - x.shape[1]
+    if pad:  # zero channels (zero products): 3 -> 4 keeps the fold at F = 8 columns, 12 -> 16 at F = 2
+        x = torch.nn.functional.pad(x, (0, 0, 0, 0, 0, pad))
+        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, pad))
     return MFMAFoldConv2dReLU.apply(x, w, conv.bias)

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <type_traits>
+#include <cmath>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1419,6 +1420,62 @@ __global__ __launch_bounds__(256) void temporal_maps_kernel(const char* __restri
 }
 
 // ============================================================================
+// The 4-channel BEV image of the reference's 12-channel option (src/train.py:66 "(occupancy(MONO)
+// + flow(RGB)) * series(3 steps)", gym_ffmp/envs/ffmp.py:16): [occupancy, R, G, B] per cell, the
+// occupancy of the newest frame as stored and the motion flow (cfg.flow: the covering disc's ego
+// velocity) as colour.  The reference's RGB came from BEV nodes outside its repository, so the
+// encoding is stated here (include/ffmp.h ffmp_bev_image), float32 operations in this order:
+//   R = clamp(rint(127.5 + 127.5 * (vx / vmax)), 0, 255), G the same of vy,
+//   B = clamp(rint(255 * (sqrt(vx*vx + vy*vy) / vmax)), 0, 255).
+// Elementwise and HBM-bound (3 planes read, 4 written per env); a thread does 4 consecutive
+// cells when the plane allows it (G even), else 1.
+// ============================================================================
+FFMP_DEV float flow_axis_rgb(float v, float vmax) {
+  const float q = v / vmax;
+  const float a = 127.5f * q;
+  return fminf(fmaxf(rintf(127.5f + a), 0.0f), 255.0f);
+}
+
+FFMP_DEV float flow_speed_rgb(float vx, float vy, float vmax) {
+  const float s = sqrtf(vx * vx + vy * vy);
+  const float q = s / vmax;
+  return fminf(fmaxf(rintf(255.0f * q), 0.0f), 255.0f);
+}
+
+template <bool CT, int V>
+__global__ __launch_bounds__(256) void bev_image_kernel(int64_t n, const void* __restrict__ occ, int64_t occ_env,
+                                                        const void* __restrict__ flow, int64_t plane, int32_t chunks,
+                                                        float vmax, void* __restrict__ out, int64_t out_env) {
+  const int64_t e = blockIdx.x / chunks;
+  const int64_t q0 = ((int64_t)(blockIdx.x - e * chunks) * 256 + threadIdx.x) * V;
+  if (e >= n || q0 >= plane) return;
+  float o[V], fx[V], fy[V];
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int64_t q = q0 + u;
+    if (CT) {
+      o[u] = (float)static_cast<const uint8_t*>(occ)[e * occ_env + q];
+      fx[u] = (float)static_cast<const _Float16*>(flow)[e * 2 * plane + q];
+      fy[u] = (float)static_cast<const _Float16*>(flow)[e * 2 * plane + plane + q];
+    } else {
+      o[u] = static_cast<const float*>(occ)[e * occ_env + q];
+      fx[u] = static_cast<const float*>(flow)[e * 2 * plane + q];
+      fy[u] = static_cast<const float*>(flow)[e * 2 * plane + plane + q];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const float c[4] = {o[u], flow_axis_rgb(fx[u], vmax), flow_axis_rgb(fy[u], vmax), flow_speed_rgb(fx[u], fy[u], vmax)};
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+      const int64_t at = e * out_env + ch * plane + q0 + u;
+      if (CT) static_cast<uint8_t*>(out)[at] = (uint8_t)c[ch];
+      else static_cast<float*>(out)[at] = c[ch];
+    }
+  }
+}
+
+// ============================================================================
 // C ABI
 // ============================================================================
 namespace {
@@ -1834,6 +1891,36 @@ int ffmp_temporal_maps(int64_t n, const void* frames, const int64_t* lag_offset,
   hipLaunchKernelGGL(temporal_maps_kernel, dim3((unsigned)(n * k * chunks)), dim3(256), 0, (hipStream_t)stream,
                      (const char*)frames, lag, k, env_b, plane_b, since, (int32_t)chunks, (char*)out);
   return check_launch("ffmp_temporal_maps");
+}
+
+int ffmp_bev_image(int64_t n, int32_t compact, const void* occ, int64_t occ_env_stride, const void* flow,
+                   int64_t plane, float vmax, void* out, int64_t out_env_stride, void* stream) {
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (plane <= 0 || occ_env_stride < plane || out_env_stride < 4 * plane)
+    return fail(FFMP_E_ARG, "plane must be > 0, occ_env_stride >= plane and out_env_stride >= 4 * plane");
+  if (!(vmax > 0.0f) || !std::isfinite(vmax)) return fail(FFMP_E_ARG, "vmax must be finite and > 0");
+  if (compact != 0 && compact != 1) return fail(FFMP_E_ARG, "compact must be 0 or 1");
+  if (n == 0) return FFMP_OK;
+  if (!occ || !flow || !out) return fail(FFMP_E_ARG, "occ/flow/out is NULL");
+  const bool quad = plane % 4 == 0 && occ_env_stride % 4 == 0 && out_env_stride % 4 == 0;
+  const int64_t per = quad ? 1024 : 256;  // cells per block
+  const int64_t chunks = (plane + per - 1) / per;
+  if (n * chunks > 0x7fffffffLL) return fail(FFMP_E_ARG, "too many blocks for one launch");
+  const dim3 grid((unsigned)(n * chunks));
+  hipStream_t s = (hipStream_t)stream;
+  if (compact && quad)
+    hipLaunchKernelGGL((bev_image_kernel<true, 4>), grid, dim3(256), 0, s, n, occ, occ_env_stride, flow, plane,
+                       (int32_t)chunks, vmax, out, out_env_stride);
+  else if (compact)
+    hipLaunchKernelGGL((bev_image_kernel<true, 1>), grid, dim3(256), 0, s, n, occ, occ_env_stride, flow, plane,
+                       (int32_t)chunks, vmax, out, out_env_stride);
+  else if (quad)
+    hipLaunchKernelGGL((bev_image_kernel<false, 4>), grid, dim3(256), 0, s, n, occ, occ_env_stride, flow, plane,
+                       (int32_t)chunks, vmax, out, out_env_stride);
+  else
+    hipLaunchKernelGGL((bev_image_kernel<false, 1>), grid, dim3(256), 0, s, n, occ, occ_env_stride, flow, plane,
+                       (int32_t)chunks, vmax, out, out_env_stride);
+  return check_launch("ffmp_bev_image");
 }
 
 #ifdef FFMP_TRACE

@@ -19,7 +19,10 @@ input_channels (train.py:66-69): 2 (default, the configuration train.py runs) = 
 option comments describe them.  temporal_maps=True instead takes make_temporal_maps' code path for
 a mono BEV image (train.py:474-486: map_memory holds INPUT_CHANNELS frames): input_channels = k
 frames, oldest first, served from the env's frame ring (FFMPVec.temporal_maps, k <= frame_window)
-and re-rastered by the replay memory (ReplayMemory(series=k)).
+and re-rastered by the replay memory (ReplayMemory(series=k)).  input_channels=12 is the option
+comment's "(occupancy(MONO) + flow(RGB)) * series(3 steps)" (train.py:66): three 4-channel BEV
+images [occupancy, R, G, B] from an env built with FFMPVec(bev_series=3) (FFMPVec.bev_maps; the RGB
+encoding is include/ffmp.h ffmp_bev_image's), replayed by ReplayMemory(series=3, bev=True).
 
 amp=True (not the reference's arithmetic, opt-in): the Q-network forwards (acting, replay and
 target) run under torch.autocast bfloat16 — the convolutions on the MFMA units in bf16, fp32
@@ -62,7 +65,14 @@ class Brain:
         # newest frame, 3 = newest frame + flow xy (needs the env's flow planes)
         self.input_channels = int(input_channels)
         self.temporal_maps = bool(temporal_maps)
-        if self.temporal_maps:
+        self.bev = self.input_channels == 12
+        if self.bev:
+            if self.temporal_maps:
+                raise ValueError("input_channels=12 is the BEV series (occupancy + RGB flow x 3 steps); "
+                                 "temporal_maps is the mono-frame series")
+            if getattr(env, "bev", None) is None or env.bev_series < 3:
+                raise ValueError("input_channels=12 needs FFMPVec(..., FFMPConfig(flow=True), bev_series=3)")
+        elif self.temporal_maps:
             if not 1 <= self.input_channels <= env.max_temporal_frames:
                 raise ValueError(f"temporal_maps: input_channels must be in [1, {env.max_temporal_frames}] for this "
                                  f"env (frame_window={env.frame_window}, ring={env.ring}; a wrapping ring holds "
@@ -72,8 +82,8 @@ class Brain:
                 raise ValueError("input_channels=3 needs an env with FFMPConfig(flow=True)")
             if self.input_channels not in (1, 2, 3):
                 raise ValueError("input_channels must be 1, 2 or 3")
-        series = self.input_channels if self.temporal_maps else 2
-        self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed, series=series)
+        series = 3 if self.bev else self.input_channels if self.temporal_maps else 2
+        self.memory = ReplayMemory(env, max(int(capacity), env.num_envs), seed=seed, series=series, bev=self.bev)
         g = env.cfg.grid
         with torch.random.fork_rng(devices=[]):  # seeded init without touching the caller's RNG
             torch.manual_seed(seed)
@@ -89,7 +99,7 @@ class Brain:
         self.gen.manual_seed(int(seed) + 1)
 
     def _q(self, net: Network, coupling: str, sm, sg, sv, st, flow=None):
-        if self.temporal_maps:  # already the k frames
+        if self.temporal_maps or self.bev:  # already the k frames / the 12 BEV channels
             sm = sm.float() if sm.dtype == torch.uint8 else sm
         else:
             sm = map_channels(sm, flow, self.input_channels)  # uint8 frames (u8f16 layout) -> float 0 / 255
@@ -108,6 +118,8 @@ class Brain:
         n = obs["state_m"].shape[0]
         if self.temporal_maps:
             obs = dict(obs, state_m=self.env.temporal_maps(self.input_channels))
+        elif self.bev:
+            obs = dict(obs, state_m=self.env.bev_maps(3))
         epsilon = 0.5 * (1.0 / (episode.to(torch.float64) + 1.0))
         u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
         self.main_q_network.eval()

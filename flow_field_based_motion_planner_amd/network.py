@@ -97,9 +97,9 @@ def map_channels(state_m: torch.Tensor, flow: "torch.Tensor | None", channels: i
       1  only temporal_bev_image: the newest frame (:68)
       3  (occupancy(MONO) + flow(xy)) * series(1 steps) (:67): the newest frame, then the BEV
          motion-flow planes (FFMPVec with cfg.flow: per-cell ego velocity of the covering disc)
-    (:66's 12 channels, occupancy + RGB flow over 3 steps, need an RGB encoding of the flow that the
-    reference's BEV nodes defined outside the repository: not offered.)  uint8 frames (the compact
-    layout) come back as float with the same 0 / 255 values."""
+    (:66's 12 channels, occupancy + RGB flow over 3 steps, are a series, not a view of one
+    observation: FFMPVec(bev_series=3).bev_maps() / Brain(input_channels=12).)  uint8 frames (the
+    compact layout) come back as float with the same 0 / 255 values."""
     if state_m.dtype == torch.uint8:
         state_m = state_m.float()
     if channels == 2:
@@ -110,5 +110,6 @@ def map_channels(state_m: torch.Tensor, flow: "torch.Tensor | None", channels: i
         if flow is None:
             raise ValueError("3 map channels need the flow planes (FFMPConfig(flow=True))")
         return torch.cat((state_m[:, 1:2], flow.float()), 1)  # binary16 flow (u8f16 layout) -> float
-    raise ValueError(f"map channels must be 1, 2 or 3 (train.py:66-69 without the RGB option), got {channels}")
+    raise ValueError(f"map channels must be 1, 2 or 3 (train.py:67-69; the 12-channel option is "
+                     f"FFMPVec.bev_maps), got {channels}")
 

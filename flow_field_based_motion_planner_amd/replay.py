@@ -29,6 +29,12 @@ record d steps back, clamped to the episode start (the last frame is the older f
 k-2 steps back: k-1 raster launches write k frames per sample).  The memory keeps the k-2 previous
 records of every env itself (push_begin must see every step); a transition pushed less than k-2
 steps after the memory was created sees its deepest lags clamped to the oldest record it has.
+
+bev=True (the 12-channel option, train.py:66: "(occupancy(MONO) + flow(RGB)) * series(3 steps)";
+FFMPVec(bev_series=k).bev_maps): the maps are k 4-channel BEV images [occupancy, R, G, B], oldest
+first (include/ffmp.h ffmp_bev_image).  The lag-d image needs the flow of the record d steps back,
+so a transition keeps the k-1 records before its state; sample() rasters each lag's record (newest
+frame + flow planes) and colours it into its 4 channels: 2k raster + 2k colour launches per batch.
 """
 from __future__ import annotations
 
@@ -36,6 +42,7 @@ import ctypes as C
 from collections import namedtuple
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _abi
@@ -51,7 +58,7 @@ class ReplayMemory:
     sample() materialises the map stacks with the env's raster kernel (state_m / observe_m
     f32 (B,2,G,G); with `potential=True` also the potential planes (B,G,G) of both sides)."""
 
-    def __init__(self, env, capacity: int, seed: int = 0, series: int = 2):
+    def __init__(self, env, capacity: int, seed: int = 0, series: int = 2, bev: bool = False):
         if not getattr(env, "keep_terminal", False):
             raise ValueError("ReplayMemory needs FFMPVec(..., keep_terminal=True) (terminal records of done envs)")
         if capacity < env.num_envs:
@@ -70,7 +77,13 @@ class ReplayMemory:
         self.series = int(series)
         if not 1 <= self.series <= _abi.MAX_SERIES:
             raise ValueError(f"series must be in [1, {_abi.MAX_SERIES}]")
-        H = max(self.series - 2, 0)
+        self.bev = bool(bev)
+        if self.bev and not self.cfg.flow:
+            raise ValueError("bev=True needs an env with FFMPConfig(flow=True)")
+        # the mono series' oldest frame is the older frame of record r_t-k+2; a BEV image needs
+        # that record's own flow, so one more record back
+        H = self.series - 1 if self.bev else max(self.series - 2, 0)
+        self._H = H
         # series > 2: records r_t-1 .. r_t-k+2 of the state, its steps since reset, and every env's
         # last k-2 records (newest first; `_seen` steps of them are real)
         self.s_hist = torch.zeros(self.capacity, H, R, dtype=torch.float32, device=dev) if H else None
@@ -107,7 +120,7 @@ class ReplayMemory:
         env = env or self.env
         n = env.num_envs
         small = torch.cat([env.state_g, env.state_v, env.state_t], dim=1)
-        H = self.series - 2
+        H = self._H
         if H > 0:
             since = env.t.clamp(max=self._seen)
         for dst, src, cnt in self._slots(n):
@@ -181,6 +194,34 @@ class ReplayMemory:
             self._raster(rec, sm, pot if d == 0 else None, flow if d == 0 else None, pos=k - 2 - d,
                          newest_only=not full)
 
+    def _bev_planes(self, key: str, B: int, potential: bool):
+        G, k = self.cfg.grid, self.series
+        want = (B, potential)
+        if self._bufs.get(key, (None,))[0] != want:
+            out = torch.empty(B, 4 * k, G, G, dtype=torch.float32, device=self.device)
+            sm = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device)
+            flow = torch.empty(B, 2, G, G, dtype=torch.float32, device=self.device)
+            pot = torch.empty(B, G, G, dtype=torch.float32, device=self.device) if potential else None
+            self._bufs[key] = (want, out, sm, flow, pot)
+        return self._bufs[key][1:]
+
+    def _bev_series(self, recs: torch.Tensor, since: torch.Tensor, out, sm, flow, pot) -> None:
+        """k BEV images per sample from recs (B, k, R) = records r_t, ..., r_t-k+1: the lag-d image
+        is [newest frame, flow colours] of r_t-min(d, since), written to channels 4(k-1-d) .."""
+        k, G2 = self.series, self.cfg.grid * self.cfg.grid
+        B = recs.shape[0]
+        ar = torch.arange(B, device=self.device)
+        vmax = float(np.float32(self.cfg.obst_vmax))
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        for d in range(k):
+            j = since.to(torch.int64).clamp(max=d)
+            rec = recs[ar, j].contiguous()
+            self._raster(rec, sm, pot if d == 0 else None, flow, newest_only=True)
+            dst = out.data_ptr() + 4 * (k - 1 - d) * G2 * out.element_size()
+            with torch.cuda.device(self.device):
+                _abi.check(self.lib.ffmp_bev_image(B, 0, sm[:, 1].data_ptr(), 2 * G2, flow.data_ptr(), G2, vmax, dst,
+                                                   4 * k * G2, stream), "ffmp_bev_image")
+
     def sample_indices(self, batch_size: int, replacement: bool = False) -> torch.Tensor:
         if batch_size > self.size and not replacement:
             raise ValueError(f"sample larger than population ({batch_size} > {self.size})")  # as random.sample
@@ -197,6 +238,34 @@ class ReplayMemory:
         B = idx.numel()
         s_rec = self.s_record.index_select(0, idx)
         o_rec = self.o_record.index_select(0, idx)
+        if self.bev:
+            s_out, s_tmp, s_flow, s_pot = self._bev_planes("bs", B, potential)
+            o_out, o_tmp, o_flow, o_pot = self._bev_planes("bo", B, potential)
+            s_since = self.s_since.index_select(0, idx) if self._H else torch.zeros(B, dtype=torch.int32,
+                                                                                    device=self.device)
+            parts = [s_rec.unsqueeze(1)] + ([self.s_hist.index_select(0, idx)] if self._H else [])
+            s_recs = torch.cat(parts, 1)                                                 # r_t .. r_t-k+1
+            o_recs = torch.cat((o_rec.unsqueeze(1), s_recs[:, :self.series - 1]), 1)     # r_t+1 .. r_t-k+2
+            self._bev_series(s_recs, s_since, s_out, s_tmp, s_flow, s_pot)
+            self._bev_series(o_recs, s_since + 1, o_out, o_tmp, o_flow, o_pot)
+            s_sm, o_sm = s_out, o_out
+        else:
+            s_sm, o_sm = self._sample_mono(idx, s_rec, o_rec, potential)
+            s_pot, o_pot = self._last_pot
+        ss = self.s_small.index_select(0, idx)
+        os_ = self.o_small.index_select(0, idx)
+        tr = Transition(s_sm, ss[:, 0:2], ss[:, 2:4], ss[:, 4:5], self.action.index_select(0, idx).view(B, 1),
+                        o_sm, os_[:, 0:2], os_[:, 2:4], os_[:, 4:5], self.reward.index_select(0, idx))
+        extra = {"done": self.done.index_select(0, idx), "index": idx}
+        if potential:
+            extra["potential"], extra["observe_potential"] = s_pot, o_pot
+        if self.cfg.flow and not self.bev:
+            extra["flow"], extra["observe_flow"] = self._last_flow
+        return tr, extra
+
+    def _sample_mono(self, idx, s_rec, o_rec, potential: bool):
+        """state_m / observe_m of the mono-frame series (k frames, or the [older, newest] pair)."""
+        B = idx.numel()
         s_sm, s_pot, s_flow = self._batch_planes("s", B, potential)
         o_sm, o_pot, o_flow = self._batch_planes("o", B, potential)
         if self.series > 2:
@@ -211,27 +280,20 @@ class ReplayMemory:
             self._raster(o_rec, o_sm, o_pot, o_flow)
             if self.series == 1:  # the newest frame only (a view)
                 s_sm, o_sm = s_sm[:, 1:], o_sm[:, 1:]
-        ss = self.s_small.index_select(0, idx)
-        os_ = self.o_small.index_select(0, idx)
-        tr = Transition(s_sm, ss[:, 0:2], ss[:, 2:4], ss[:, 4:5], self.action.index_select(0, idx).view(B, 1),
-                        o_sm, os_[:, 0:2], os_[:, 2:4], os_[:, 4:5], self.reward.index_select(0, idx))
-        extra = {"done": self.done.index_select(0, idx), "index": idx}
-        if potential:
-            extra["potential"], extra["observe_potential"] = s_pot, o_pot
-        if self.cfg.flow:
-            extra["flow"], extra["observe_flow"] = s_flow, o_flow
-        return tr, extra
+        self._last_pot, self._last_flow = (s_pot, o_pot), (s_flow, o_flow)
+        return s_sm, o_sm
 
     _SD = ("s_record", "o_record", "s_small", "o_small", "action", "reward", "done", "s_hist", "s_since", "_env_hist")
 
     def state_dict(self) -> dict:
         sd = {k: getattr(self, k).clone() for k in self._SD if getattr(self, k) is not None}
-        sd.update(index=self.index, size=self.size, series=self.series, seen=self._seen)
+        sd.update(index=self.index, size=self.size, series=self.series, seen=self._seen, bev=self.bev)
         return sd
 
     def load_state_dict(self, sd: dict) -> None:
-        if int(sd.get("series", 2)) != self.series:
-            raise ValueError(f"state_dict of a series={sd.get('series', 2)} memory, this one has {self.series}")
+        if int(sd.get("series", 2)) != self.series or bool(sd.get("bev", False)) != self.bev:
+            raise ValueError(f"state_dict of a series={sd.get('series', 2)} bev={sd.get('bev', False)} memory, "
+                             f"this one has series={self.series} bev={self.bev}")
         for k in self._SD:
             if getattr(self, k) is not None:
                 getattr(self, k).copy_(sd[k])

@@ -83,6 +83,11 @@ class FFMPVec:
             with the same 0/255 values (`state_m.float()` is the f32 layout bit for bit) and the
             potential plane as float16 (the float32 value rounded to nearest even): 3 instead of
             8 bytes per cell of a step's raster.  With cfg.flow the flow planes are float16 too.
+        bev_series: k > 0 (needs cfg.flow): also keep the last k 4-channel BEV images [occupancy,
+            R, G, B] of every env (ffmp_bev_image: the newest frame and its motion flow as colour),
+            a ring `bev` (k, N, 4, G, G) written after every step / reset; bev_maps() is the input of
+            the reference's 12-channel option (train.py:66: "(occupancy(MONO) + flow(RGB)) *
+            series(3 steps)", k = 3).  One extra elementwise launch per step.
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -91,7 +96,7 @@ class FFMPVec:
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
                  frame_window: Optional[int] = None, seamless: Optional[bool] = None,
                  fused: Optional[bool] = None, tuning: Optional[dict] = None, obs_format: str = "f32",
-                 hbm_budget: Optional[int] = None):
+                 hbm_budget: Optional[int] = None, bev_series: int = 0):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -139,6 +144,19 @@ class FFMPVec:
         self._hist = []
         self._hist_from_reset = False
         self._alloc()
+        self.bev_series = int(bev_series)
+        self.bev = None
+        if self.bev_series:
+            if not self.cfg.flow:
+                raise ValueError("bev_series needs FFMPConfig(flow=True) (the flow planes it colours)")
+            if not 1 <= self.bev_series <= _abi.MAX_SERIES:
+                raise ValueError(f"bev_series must be in [1, {_abi.MAX_SERIES}]")
+            G = self.cfg.grid
+            self.bev = torch.zeros(self.bev_series, self.num_envs, 4, G, G, dtype=self._frame_dtype,
+                                   device=self.device)
+        self._bev_pos = 0       # ring slot of the newest image
+        self._bev_hist = []     # slots of the newest images, newest first (as _hist)
+        self._bev_from_reset = False
         G2 = self.cfg.grid * self.cfg.grid
         if pipeline is None:
             pipeline = 1  # measured: no net gain on MI355X (profiles/r01_pipeline.txt, r03b_pipeline.txt)
@@ -922,6 +940,63 @@ class FFMPVec:
         so after the first wrap it holds W - 1 distinct frames)."""
         return self.frame_window - 1 if self.ring == "wrap" else self.frame_window
 
+    def _bev_push(self, advance: bool, restart: bool = False) -> None:
+        """Write the current BEV image of every env into the ring (bev_series): a new slot after a
+        step (advance), the current one again after a re-raster or masked reset, slot 0 after a full
+        reset (restart: every env's older lags are clamped away)."""
+        if self.bev is None:
+            return
+        S = self.bev.shape[0]
+        if restart:
+            self._bev_pos, self._bev_hist, self._bev_from_reset = 0, [0], True
+        elif advance:
+            self._bev_pos = (self._bev_pos + 1) % S
+            self._bev_hist = ([self._bev_pos] + self._bev_hist)[:S]
+        elif not self._bev_hist:
+            self._bev_hist = [self._bev_pos]
+        G2 = self.cfg.grid * self.cfg.grid
+        sm = self.state_m
+        with torch.cuda.device(self.device):
+            self._bev_launch(sm, G2)
+
+    def _bev_launch(self, sm: torch.Tensor, G2: int) -> None:
+        _abi.check(self.lib.ffmp_bev_image(self.num_envs, 1 if self.obs_format == "u8f16" else 0,
+                                           sm[:, 1].data_ptr(), sm.stride(0), self.flow.data_ptr(), G2,
+                                           float(np.float32(self.cfg.obst_vmax)), self.bev[self._bev_pos].data_ptr(),
+                                           4 * G2, self._stream()), "ffmp_bev_image")
+
+    def bev_maps(self, k: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """make_temporal_maps over the last k 4-channel BEV images (bev_series): (N, 4k, G, G),
+        oldest image first, each [occupancy, R, G, B] (include/ffmp.h ffmp_bev_image), every env's
+        lags clamped to its episode start as in temporal_maps (is_first refills map_memory) — the
+        reference's INPUT_CHANNELS = 12 option at k = 3 (train.py:66, ffmp.py:16).  Gathered by
+        ffmp_temporal_maps from the ring into `out` (or a new tensor; frames' dtype)."""
+        self._check_open()
+        if self.bev is None:
+            raise RuntimeError("bev_maps() needs FFMPVec(..., bev_series=k)")
+        S = self.bev.shape[0]
+        k = S if k is None else int(k)
+        if not 1 <= k <= S:
+            raise ValueError(f"k must be in [1, {S}] (bev_series={S})")
+        if self._needs_reset:
+            raise RuntimeError("call reset() before bev_maps()")
+        if len(self._bev_hist) < k and not self._bev_from_reset:
+            raise RuntimeError(f"the BEV ring holds {len(self._bev_hist)} known images since the last reload; "
+                               f"bev_maps({k}) needs {k} (step {k - len(self._bev_hist)} more times, or reset())")
+        N, G = self.num_envs, self.cfg.grid
+        plane = 4 * G * G
+        hist = self._bev_hist
+        offs = [hist[min(d, len(hist) - 1)] * N * plane for d in range(k)]
+        if out is None:
+            out = torch.empty(N, 4 * k, G, G, dtype=self.bev.dtype, device=self.device)
+        elif out.shape != (N, 4 * k, G, G) or out.dtype != self.bev.dtype or not out.is_contiguous() \
+                or out.device != self.device:
+            raise ValueError(f"out must be a contiguous {self.bev.dtype} tensor of shape {(N, 4 * k, G, G)} on {self.device}")
+        lag = (C.c_int64 * k)(*offs)
+        _abi.check(self.lib.ffmp_temporal_maps(N, self.bev.data_ptr(), lag, k, plane, plane, self._fes,
+                                               self.t.data_ptr(), out.data_ptr(), self._stream()), "ffmp_temporal_maps")
+        return out
+
     def temporal_maps(self, k: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """make_temporal_maps (src/train.py:474-486) over the last k frames: (N, k, G, G), oldest
         first, each env's lags clamped to its episode start (is_first refills the reference's
@@ -1024,6 +1099,7 @@ class FFMPVec:
                                            C.byref(self._state_c), C.byref(self._obs_c), s), "ffmp_reset")
             self._raster_launch(True, m)
             self._mask_keepalive = m
+            self._bev_push(advance=False, restart=mask is None)
         self._needs_reset = False
         return self._obs_out(copy)
 
@@ -1050,6 +1126,7 @@ class FFMPVec:
         self._check_open()
         m = None if mask is None else mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
         self._raster_launch(True, m)
+        self._bev_push(advance=False)
 
     def _next_window(self) -> bool:
         """Slide the [older, newest] pair by one slot for the next raster; True if that raster
@@ -1146,6 +1223,7 @@ class FFMPVec:
             else:
                 self.step_state(actions)
                 self.raster_step(timing)
+            self._bev_push(advance=True)
         info = {"is_goal": self.is_goal, "collision": self.collision, "truncated": self.truncated,
                 "step": self.t, "episode": self.episode}
         if copy:
@@ -1229,6 +1307,7 @@ class FFMPVec:
         self._state_c = self._obs_c = self._out_c = None
         self._slices = []
         self._arena_buf = None
+        self.bev = None
         had_ring = self.ring == "seamless"
         self._ring = None  # the seamless ring's pieces return to the process pool ...
         torch.cuda.empty_cache()
@@ -1238,6 +1317,7 @@ class FFMPVec:
             _abi.ring_pool_trim(self.device.index, 0)  # ... and their memory to the device
 
     _closed = False
+    bev = None  # the BEV image ring (bev_series); a class default: _alloc's HBM accounting runs first
 
     def _check_open(self) -> None:
         if self._closed:
@@ -1286,6 +1366,7 @@ class FFMPVec:
         self.raster()
         self._hist, self._hist_from_reset = [], False  # older frames than the pair are not restored
         self._note_window(True)
+        self._bev_hist, self._bev_from_reset = [self._bev_pos], False  # likewise older BEV images
         self._needs_reset = False
 
     def hbm_bytes(self) -> int:
@@ -1295,7 +1376,7 @@ class FFMPVec:
         if self.ring == "seamless" and getattr(self, "_ring", None) is not None:
             ring = self.frame_window * self._ring.slot_stride
         if self._arena_buf is not None:
-            return self._arena_buf.numel() + ring
+            return self._arena_buf.numel() + ring + (self.bev.numel() * self.bev.element_size() if self.bev is not None else 0)
         return ring + sum(t.numel() * t.element_size() for t in vars(self).values()
                           if isinstance(t, torch.Tensor) and not (ring and t is self.frames))
 

@@ -22,6 +22,8 @@
  *                          (src/train.py:474-486) kept in place (optional helper)
  *   ffmp_temporal_maps  -> make_temporal_maps over INPUT_CHANNELS = k mono frames
  *                          (src/train.py:66-69, 474-486) served from the frame ring
+ *   ffmp_bev_image      -> the (occupancy + flow(RGB)) image of the 12-channel option
+ *                          (src/train.py:66, src/gym_ffmp/envs/ffmp.py:16)
  *   ffmp_raster         -> external /bev_flow_estimator + /temporal_bev_publisher
  *                          (src/train.py:116-121, make_temporal_maps :474-486)
  *   ffmp_reward_done    -> FFMP.rewarder / rewarder2 / reward_calculator /
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 6
+#define FFMP_ABI_VERSION 7
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -380,6 +382,20 @@ int ffmp_episode_update(int64_t n, const ffmp_out_t* out, int32_t window, int32_
 #define FFMP_MAX_SERIES 16
 int ffmp_temporal_maps(int64_t n, const void* frames, const int64_t* lag_offset, int32_t k, int64_t env_stride,
                        int64_t plane, int32_t elem_bytes, const int32_t* since, void* out, void* stream);
+
+/* The 4-channel BEV image [occupancy, R, G, B] of the reference's 12-channel option
+ * (src/train.py:66 "INPUT_CHANNELS = 12 #[channel] = (occupancy(MONO) + flow(RGB)) * series(3
+ * steps)", src/gym_ffmp/envs/ffmp.py:16): the series of 3 such images is ffmp_temporal_maps over a
+ * ring of them (plane = 4*G*G).  occ: the newest frame of env e at occ + e * occ_env_stride
+ * (state_m's newest plane); flow: the (n, 2, plane) motion-flow planes of cfg.flow (ego vx, vy);
+ * out: channel c of env e at out + e * out_env_stride + c * plane.  compact 0: float32 occ / flow /
+ * out, compact 1 (FFMP_OBS_U8F16): uint8 occ and out, binary16 flow.  The reference's RGB flow
+ * image came from BEV nodes outside its repository; the encoding here (float32, in this order):
+ *   R = clamp(rint(127.5 + 127.5 * (vx / vmax)), 0, 255), G = the same of vy,
+ *   B = clamp(rint(255 * (sqrt(vx*vx + vy*vy) / vmax)), 0, 255)   (rint: half to even)
+ * — zero velocity is (128, 128, 0); vmax = the obstacle speed bound (FFMPConfig.obst_vmax). */
+int ffmp_bev_image(int64_t n, int32_t compact, const void* occ, int64_t occ_env_stride, const void* flow,
+                   int64_t plane, float vmax, void* out, int64_t out_env_stride, void* stream);
 
 /* Seamless frame ring — an optional allocation helper (the step / raster entry points above
  * still never allocate).  The temporal stack of make_temporal_maps (src/train.py:474-486)

@@ -132,7 +132,7 @@ def test_conv_dilated_matches_float64(B, H, W, KH, KW, dx, N):
     assert not bool(((y.double() - ref).abs() > 5e-5 * absref + 1e-6).any())
 
 
-@pytest.mark.parametrize("C", [2, 1, 3])
+@pytest.mark.parametrize("C", [2, 1, 3, 12])
 def test_folded_conv1_against_float64(C):
     """The reference Network's conv1 (C map channels -> 32, k = 32, 100^2 -> 69^2; train.py:234)
     with its kernel columns folded into 32 channels: forward vs float64 of the same bf16 operands
@@ -142,7 +142,7 @@ def test_folded_conv1_against_float64(C):
     conv = torch.nn.Conv2d(C, 32, kernel_size=32).to(DEV)
     assert fold_supported(conv)
     x = (torch.rand((3, C, 100, 100), device=DEV, generator=g) > 0.85).float() * 255
-    y = fold_conv_relu(conv, x)  # C = 3: a zero fourth channel
+    y = fold_conv_relu(conv, x)  # C = 3: a zero fourth channel; C = 12: four zero channels (F = 2)
     x64 = x.double()
     w64 = conv.weight.detach().to(torch.bfloat16).double().requires_grad_(True)
     b64 = conv.bias.detach().double().requires_grad_(True)

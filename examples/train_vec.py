@@ -47,8 +47,8 @@ def main():
                     help="with --amp: conv2-conv4 through MIOpen instead of the MFMA kernel (conv_mfma.py)")
     ap.add_argument("--channels-last", action="store_true", help="NHWC Q-networks (Brain(channels_last=True))")
     ap.add_argument("--input-channels", type=int, default=2,
-                    help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy; "
-                         "with --temporal-maps: that many frames")
+                    help="map input (train.py:66-69): 2 = [older, newest], 1 = newest, 3 = newest + flow xy, "
+                         "12 = (occupancy + RGB flow) x 3 steps (FFMPVec.bev_maps); with --temporal-maps: that many frames")
     ap.add_argument("--temporal-maps", action="store_true",
                     help="make_temporal_maps over --input-channels mono frames (train.py:474-486), from the frame ring")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
@@ -57,11 +57,12 @@ def main():
     dev = torch.device("cuda:0")
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
     cfg = FFMPConfig(grid=100, n_obst=4, n_beams=180, moving=True, max_steps=200, seed=args.seed,
-                     flow=args.input_channels == 3 and not args.temporal_maps)
+                     flow=args.input_channels in (3, 12) and not args.temporal_maps)
     # k + 1 slots: enough on a wrapping ring too (the fallback on devices without HIP VMM), which
     # holds W - 1 distinct frames once it has wrapped (FFMPVec.max_temporal_frames)
     window = max(args.input_channels + 1, 3) if args.temporal_maps else None
-    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format, frame_window=window)
+    env = FFMPVec(args.envs, cfg, device=dev, keep_terminal=True, obs_format=args.obs_format, frame_window=window,
+                  bev_series=3 if args.input_channels == 12 and not args.temporal_maps else 0)
     brain = Brain(env, capacity=args.capacity, batch_size=args.batch, seed=args.seed, amp=args.amp,
                   mfma=False if args.no_mfma else None,
                   channels_last=args.channels_last, input_channels=args.input_channels,

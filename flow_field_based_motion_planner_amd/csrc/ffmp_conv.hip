@@ -91,8 +91,21 @@ __device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4
 // border: ~12 % of its work).  Kernel column kx reads input column xp + kx * dx (dx > 1: the
 // x-dilated form a 1- or 2-channel convolution takes after its kernel columns are folded into
 // channels, conv_mfma.fold_input).
+// B fragments: 1 = the next tap's loaded into a copy that replaces the current set (the copy made
+// every tap wait for them after one k-step of MFMAs: vmcnt(0) at the top of each tap), 2 = two sets
+// that swap roles (the kx loop unrolled by two), each waited for a whole tap after its request.
+// 0 (default): 2 for one channel block (NB = 1: the data gradient 3.20 -> 3.10-3.15 ms, the folded
+// conv1 0.414 -> 0.393 ms at B = 256), 1 for two (NB = 2: conv2's forward has 233 of its 256
+// registers in use and ran 1.37 -> 1.67 ms with the second set; profiles/r04q_conv_prefetch.txt).
+#ifndef FFMP_CONV_BAHEAD
+#define FFMP_CONV_BAHEAD 0
+#endif
+
+#ifndef FFMP_CONV_FWD_OCC
+#define FFMP_CONV_FWD_OCC 2  // workgroups per CU the forward kernel is compiled for
+#endif
 template <int C, int NB, int MBW, bool PAD>
-__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
+__global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -147,16 +160,21 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
     for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x16{};
 
   // B fragments of the wave's first tap (wk_lo, 0); from then on loaded one tap ahead (the active
-  // kernel rows [wk_lo, wk_hi] are consecutive)
-  bf16x8 bcur[NB][C / 16];
-  {
-    const int t0 = min(wk_lo, KH - 1) * KW;
+  // kernel rows [wk_lo, wk_hi] are consecutive, so the tap after t is t + 1, up to the wave's last
+  // tap, which later loads re-read)
+  const int t_last = min(wk_hi, KH - 1) * KW + KW - 1;
+  auto load_b = [&](int t, bf16x8 (&dst)[NB][C / 16]) {
+    t = min(t, t_last);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int s = 0; s < C / 16; ++s)
-        bcur[nb][s] = *(const bf16x8*)(w + ((size_t)(t0 * N + nb * 32 + r) * C + s * 16 + h * 8));
-  }
+        dst[nb][s] = *(const bf16x8*)(w + ((size_t)(t * N + nb * 32 + r) * C + s * 16 + h * 8));
+  };
+  constexpr int kBAhead = FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
+  bf16x8 bcur[NB][C / 16];
+  bf16x8 bnx[NB][C / 16];  // kBAhead 2: the ping-pong partner of bcur
+  load_b(min(wk_lo, KH - 1) * KW, bcur);
 
   for (int ky = ky_lo; ky <= ky_hi; ++ky) {
     uint4 nrow[4];
@@ -166,16 +184,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
       int aoff[MBW];
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
-      for (int kx = 0; kx < KW; ++kx) {
-        // the next tap: (ky, kx + 1), else (ky + 1, 0) while the wave has rows left (the last
-        // tap re-reads its own)
-        const int tn = kx + 1 < KW ? ky * KW + kx + 1 : (ky < wk_hi ? (ky + 1) * KW : ky * KW + kx);
-        bf16x8 bnext[NB][C / 16];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int s = 0; s < C / 16; ++s)
-            bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
+      // the MFMAs of tap (ky, kx) with its B fragments
+      auto tap = [&](int kx, const bf16x8 (&bt)[NB][C / 16]) {
         // the lane's column of each block, or the zero column outside the tensor (PAD)
         int abase[MBW];
 #pragma unroll
@@ -192,12 +202,37 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
           for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb)
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bcur[nb][s], acc[mb][nb], 0, 0, 0);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bt[nb][s], acc[mb][nb], 0, 0, 0);
         }
+      };
+      if constexpr (kBAhead == 2) {
+        // two taps per trip, B in two register sets that swap roles without copies: the next tap's
+        // fragments are requested before this tap's MFMAs and waited for a whole tap later
+        int kx = 0;
+        for (; kx + 1 < KW; kx += 2) {
+          load_b(ky * KW + kx + 1, bnx);
+          tap(kx, bcur);
+          load_b(ky * KW + kx + 2, bcur);
+          tap(kx + 1, bnx);
+        }
+        if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
+          load_b(ky * KW + kx + 1, bnx);
+          tap(kx, bcur);
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+          for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-          for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
+            for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnx[nb][s];
+        }
+      } else {
+        for (int kx = 0; kx < KW; ++kx) {
+          bf16x8 bnext[NB][C / 16];
+          load_b(ky * KW + kx + 1, bnext);
+          tap(kx, bcur);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
+        }
       }
     }
     if (more) store_row_lds<C>(lds + ((yl + ky + 1) % RING) * pitch, chunks, nrow);

@@ -149,7 +149,7 @@ class MFMAConv2dReLU(torch.autograd.Function):
         if need[1]:  # on the matrix cores too: [KH][KW][N][C] -> torch's [N][C][KH][KW]
             gw = conv2d_wgrad_nhwc(g, xb, weight.shape[2], weight.shape[3]).permute(2, 3, 0, 1).to(weight.dtype)
         if ctx.has_bias and need[2]:
-            gb = g.float().sum((0, 1, 2))
+            gb = g.sum((0, 1, 2), dtype=torch.float32)  # fp32 accumulation, no fp32 copy of g
         return gx, gw, gb
 
 
@@ -239,7 +239,7 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
             gwf = conv2d_wgrad_nhwc(g, fold_input(x, F), KH, KW // F, dx=F)  # [KH][KW/F][N][F*C]
             gw = gwf.view(KH, KW // F, N, F, Cc).permute(2, 4, 0, 1, 3).reshape(N, Cc, KH, KW).to(weight.dtype)
         if ctx.has_bias and need[2]:
-            gb = g.float().sum((0, 1, 2))
+            gb = g.sum((0, 1, 2), dtype=torch.float32)  # fp32 accumulation, no fp32 copy of g
         return gx, gw, gb
 
 

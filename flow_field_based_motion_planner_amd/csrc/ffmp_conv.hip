@@ -530,6 +530,12 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
 #ifndef FFMP_WGRAD_TW_3264
 #define FFMP_WGRAD_TW_3264 8
 #endif
+// 1: each k-step's operand reads are issued during the previous k-step's MFMAs (two register sets);
+// -1: that for the 32 -> 64 kernel only (the smaller ones spill with it); 0 (default): not — the
+// 32 -> 64 weight gradient ran 1.75-1.77 -> 1.82-1.83 ms with it (profiles/r04s_wgrad_prefetch.txt)
+#ifndef FFMP_WGRAD_PREFETCH
+#define FFMP_WGRAD_PREFETCH 0
+#endif
 template <int C, int N, int TW>
 __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
                                                             float* __restrict__ part, int B, int H, int W, int KH,
@@ -605,10 +611,9 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
       pr[u] = p / Wo;
       pc[u] = p - pr[u] * Wo;
     }
-    for (int k0 = 0; k0 < Ps; k0 += 16) {
-      // each operand fragment = two transposing reads (k rows 8h + 4u .. +4), joined as whole
-      // vectors (element-wise assembly of the 4 x 16-bit results miscompiles: ROCm 7.2)
-      s16x4 ar[NB][2], br[TW][CB][2];
+    // each operand fragment = two transposing reads (k rows 8h + 4u .. +4), joined as whole
+    // vectors (element-wise assembly of the 4 x 16-bit results miscompiles: ROCm 7.2)
+    auto fetch = [&](int k0, s16x4 (&ar)[NB][2], s16x4 (&br)[TW][CB][2]) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int p = k0 + 8 * h + 4 * u + q;
@@ -637,6 +642,8 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
         pc[u] = c;
         pr[u] = rr;
       }
+    };
+    auto mma = [&](const s16x4 (&ar)[NB][2], const s16x4 (&br)[TW][CB][2]) {
       bf16x8 a[NB], bb[TW][CB];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
@@ -654,6 +661,26 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb)
             acc[t][nb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[nb], bb[t][cb], acc[t][nb][cb], 0, 0, 0);
+    };
+    constexpr bool kPrefetch = FFMP_WGRAD_PREFETCH < 0 ? TW * NB * CB >= 16 : FFMP_WGRAD_PREFETCH != 0;
+    if constexpr (kPrefetch) {
+      // the next k-step's fragments are read while this one's MFMAs run (two register sets, the loop
+      // unrolled by two so they swap roles without copies)
+      s16x4 arA[NB][2], brA[TW][CB][2], arB[NB][2], brB[TW][CB][2];
+      fetch(0, arA, brA);
+      for (int k0 = 0; k0 < Ps; k0 += 32) {
+        fetch(k0 + 16, arB, brB);
+        mma(arA, brA);
+        if (k0 + 16 >= Ps) break;
+        fetch(k0 + 32, arA, brA);
+        mma(arB, brB);
+      }
+    } else {
+      for (int k0 = 0; k0 < Ps; k0 += 16) {
+        s16x4 ar[NB][2], br[TW][CB][2];
+        fetch(k0, ar, br);
+        mma(ar, br);
+      }
     }
   }
 

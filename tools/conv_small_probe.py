@@ -1,0 +1,34 @@
+"""The Network's conv3 / conv4 forwards (64 -> 64 channels, 8 x 8 kernels: 38^2 -> 31^2 -> 24^2 ->
+17^2 -> 10^2) at B = 256 on the MFMA kernels, per shape.  FFMP_CONV_SMALL_MAX (read once per process)
+moves shapes between conv_small_kernel and the row-ring conv_fwd_kernel."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flow_field_based_motion_planner_amd.conv_mfma import conv2d_nhwc, pack_weight  # noqa: E402
+
+dev = torch.device("cuda:0")
+B = 256
+w = pack_weight(torch.randn(64, 64, 8, 8, device=dev) / 64.0)
+bias = torch.randn(64, device=dev)
+tag = os.environ.get("FFMP_CONV_SMALL_MAX", "2048")
+tot = 0.0
+for H in (38, 31, 24, 17):
+    x = torch.relu(torch.randn(B, H, H, 64, device=dev)).to(torch.bfloat16)
+    fn = lambda: conv2d_nhwc(x, w, bias, relu=True, out_dtype=torch.bfloat16)  # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    Ho = H - 7
+    flop = 2.0 * B * Ho * Ho * 64 * 64 * 64
+    tot += ms
+    print(f"small_max {tag}: {H}^2 -> {Ho}^2  {ms:.4f} ms  {flop / ms / 1e9:.0f} TFLOP/s", flush=True)
+print(f"small_max {tag}: the four shapes {tot:.4f} ms", flush=True)

@@ -1,6 +1,7 @@
 """The Network's conv3 / conv4 forwards (64 -> 64 channels, 8 x 8 kernels: 38^2 -> 31^2 -> 24^2 ->
-17^2 -> 10^2) at B = 256 on the MFMA kernels, per shape.  FFMP_CONV_SMALL_MAX (read once per process)
-moves shapes between conv_small_kernel and the row-ring conv_fwd_kernel."""
+17^2 -> 10^2) at B = 256 on the MFMA kernels, per shape.  With the probe build of tools/gpu_r04y.sh
+(FFMP_LIB=tools/_build/libffmp_sm.so), FFMP_CONV_SMALL_MAX (read once per process) moves shapes
+between conv_small_kernel and the row-ring conv_fwd_kernel; the shipped library ignores it."""
 import os
 import sys
 

@@ -184,7 +184,13 @@ def _cpu_model() -> str:
 
 
 def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):
-    """HBM bytes per raster launch from the committed rocprofv3 PMC summary, if it matches."""
+    """(HBM bytes per raster launch, the profile file it came from) from the committed rocprofv3 PMC
+    summary, if one matches this launch; (None, None) otherwise."""
+    b = _load_traffic(workload, n_envs, window, ring, fused, obs_format)
+    return b if b is not None else (None, None)
+
+
+def _load_traffic(workload, n_envs, window, ring, fused, obs_format):
     label = f"{workload}{'' if obs_format == 'f32' else '_' + obs_format}"
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{'_fused' if fused else ''}.json")
     if not os.path.exists(path):  # the one-launch and two-launch steps are profiled separately
@@ -198,7 +204,7 @@ def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool
                 or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused \
                 or d.get("obs_format", "f32") != obs_format:
             return None
-        return float(d["raster_hbm_bytes_per_launch"])
+        return float(d["raster_hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
     except Exception:  # noqa: BLE001
         return None
 
@@ -294,6 +300,37 @@ def _gather_floats(vals, world, dev, backend):
     return [o.tolist() for o in out]
 
 
+# What every rank reports after its timed region (one all_gather, never inside it): enough to
+# explain a max-over-ranks line — which rank was slow, and whether its kernel, its launch choice
+# (one- or two-launch step, raster shape) or its HBM pairing (ring slot times, the weakest accepted
+# piece pairing) made it so.  NaN = not applicable (no seamless ring, no repair timing).
+RANK_FIELDS = ("elapsed_s", "construct_s", "n_envs", "kernel_ms", "frac", "fused", "shape_cells", "shape_flags",
+               "slot_ms_min", "slot_ms_max", "pair_gbs_min")
+
+
+def rank_record(el_local: float, construct_s: float, n: int, kernel_ms: float, frac: float, env) -> list:
+    """This rank's RANK_FIELDS values (floats) from its timed loop and its FFMPVec."""
+    nan = float("nan")
+    pl = getattr(env, "placement", None) or {}
+    fused = bool(getattr(env, "fused", False))
+    sh = pl.get("shape_newest") or pl.get("shape") or {}
+    cells = nan if fused else float(sh.get("cells_per_block", nan))
+    flags = float((pl.get("fused") or {}).get("flags", nan)) if fused else float(sh.get("flags", nan))
+    meta = getattr(env, "ring_meta", None) or {}
+    slots = next((h["slot_ms"] for h in reversed(meta.get("repair") or []) if "slot_ms" in h and not h.get("reverted")),
+                 None)
+    return [float(el_local), float(construct_s), float(n), float(kernel_ms), float(frac), float(fused), cells, flags,
+            float(min(slots)) if slots else nan, float(max(slots)) if slots else nan,
+            float(meta.get("pair_gbs_min", nan) or nan)]
+
+
+def per_rank_table(rows) -> dict:
+    """Gathered rank records (rank order) -> {field: [value of rank 0, rank 1, ...]} (NaN -> None)."""
+    def clean(v):
+        return None if v != v else (int(v) if v == int(v) and abs(v) < 2 ** 53 else round(v, 5))
+    return {f: [clean(r[i]) for r in rows] for i, f in enumerate(RANK_FIELDS)}
+
+
 def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg):
     """Build one FFMPVec shard (timed: construct_s), W warm-up + K timed steps between barriers and
     synchronizes, max over ranks; the dominant kernel's launches timed with HIP events on the
@@ -348,8 +385,6 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     el_local = time.perf_counter() - t0
     env.check_errors()
     resets = int(env.episode.sum()) - int(ep0_t)  # auto-resets in the timed steps
-    per_rank = _gather_floats([el_local, construct_s, float(n)], world, dev, args.dist_backend)
-    el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
 
     # the dominant kernel — the raster, or with the one-launch step the fused env-step + raster
     # kernel: HIP events around every launch on the launch stream; algorithmic bytes per launch
@@ -366,12 +401,18 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
+    # one all_gather of every rank's record after the timed region (the max-reduce of the timings
+    # is its first column)
+    per_rank = _gather_floats(rank_record(el_local, construct_s, n, sum(r_ms) / len(r_ms), achieved / PEAK_HBM_GBS, env),
+                              world, dev, args.dist_backend)
+    el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
     n_total = int(sum(r[2] for r in per_rank))
     out = {
         "workload": name, "n_envs_total": n_total, "n_envs_per_gpu": n, "scaling": "strong" if strong else "weak",
         "value": n_total * K / el, "ms_per_step": el * 1e3 / K, "steps": K, "warmup": W,
         "per_rank_ms_per_step": [round(r[0] * 1e3 / K, 4) for r in per_rank],
         "per_rank_construct_s": [round(r[1], 2) for r in per_rank],
+        "per_rank": per_rank_table(per_rank),
         "construct_s": round(construct_s, 2), "hbm_bytes": env.hbm_bytes(),
         "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
         "pool_released_bytes": getattr(env, "pool_released_bytes", 0),
@@ -499,7 +540,8 @@ def main():
     cfg, n, strong = _leg_size(name, args, world, dev)
     K, W = args.steps, args.warmup
     leg, env = run_leg(args, name, cfg, n, rank * n, K, W, dev, world, rank, strong, True)
-    traffic = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused, args.obs_format)
+    traffic, traffic_source = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused,
+                                           args.obs_format)
     _release(env)
     env = None
 
@@ -531,7 +573,9 @@ def main():
             strong_leg.pop("per_launch_envs", None)
 
     if rank == 0:
-        rl = dict(leg["roofline"], traffic=traffic)
+        # traffic: the PMC-measured HBM bytes per launch of this launch kind, looked up from the
+        # committed rocprofv3 summary named by traffic_source (bench.py runs no counters itself)
+        rl = dict(leg["roofline"], traffic=traffic, traffic_source=traffic_source)
         out = {
             "metric": METRIC,
             "value": leg["value"],
@@ -557,6 +601,8 @@ def main():
             "per_rank_ms_per_step": leg["per_rank_ms_per_step"],
             "construct_s": leg["construct_s"],
             "per_rank_construct_s": leg["per_rank_construct_s"],
+            # every rank's kernel time, roofline fraction, launch choice and ring pairing (RANK_FIELDS)
+            "per_rank": leg["per_rank"],
             "hbm_bytes": leg["hbm_bytes"],
             "hbm_in_use_bytes": leg["hbm_in_use_bytes"],
             # HBM the process holds beyond the instance (torch context, caches); round 3 parked ~65 GB

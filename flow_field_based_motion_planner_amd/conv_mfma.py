@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes as C
 import functools
+import os
 from typing import Optional
 
 import torch
@@ -57,7 +58,8 @@ def supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
     Ho, Wo = H - KH + 1, W - KW + 1
     if C != conv.in_channels or Ho < 1 or Wo < 1:
         return False
-    return (shape_ok(0, B, H, W, C, KH, KW, N) and shape_ok(0, B, Ho, Wo, N, KH, KW, C, KH - 1)
+    return (shape_ok(0, B, H, W, C, KH, KW, N)
+            and (shape_ok(0, B, Ho, Wo, N, KH, KW, C, KH - 1) or dgrad_bm_ok(B, Ho, Wo, N, KH, KW, C))
             and shape_ok(1, B, H, W, C, KH, KW, N))
 
 
@@ -69,6 +71,46 @@ def pack_weight(w: torch.Tensor) -> torch.Tensor:
 def pack_weight_dgrad(w: torch.Tensor) -> torch.Tensor:
     """The data gradient's kernel: w'[ky][kx][c][n] = w[n][c][KH-1-ky][KW-1-kx] (bf16)."""
     return w.detach().to(torch.bfloat16).flip(2, 3).permute(2, 3, 1, 0).contiguous()
+
+
+def pack_weight_dgrad_bm(w: torch.Tensor) -> torch.Tensor:
+    """ffmp_conv2d_dgrad_bf16's kernel from torch's w [N][C][KH][KW]: w'[ky][kx][n // 8][c][n % 8] =
+    w[n][c][KH-1-ky][KW-1-kx] (bf16; n = the forward's output channel = the gradient's channel, in
+    blocks of 8 ahead of the input channel c)."""
+    N, Cc, KH, KW = w.shape
+    return (w.detach().to(torch.bfloat16).flip(2, 3).view(N // 8, 8, Cc, KH, KW)
+            .permute(3, 4, 0, 2, 1).contiguous())
+
+
+def conv2d_dgrad_nhwc(g: torch.Tensor, w_bm: torch.Tensor, out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """dx[b, Y, X, n] = sum g[b, Y+ky-(KH-1), X+kx-(KW-1), c] w'[ky, kx, c, n] (cells outside g zero):
+    the data gradient of an unpadded stride-1 convolution, 32 samples per MFMA block
+    (ffmp_conv2d_dgrad_bf16).  g NHWC bf16 [B, Hy, Wy, C], w_bm from pack_weight_dgrad_bm; returns
+    NHWC [B, Hy+KH-1, Wy+KW-1, N]."""
+    if g.dtype != torch.bfloat16 or w_bm.dtype != torch.bfloat16:
+        raise TypeError("conv2d_dgrad_nhwc takes bf16 g and packed weight")
+    if not g.is_cuda or not g.is_contiguous() or not w_bm.is_contiguous():
+        raise ValueError("conv2d_dgrad_nhwc takes contiguous device tensors")
+    B, Hy, Wy, Cg = g.shape
+    KH, KW, C8, Cn, eight = w_bm.shape
+    if C8 * eight != Cg or eight != 8:
+        raise ValueError(f"channel mismatch: g has {Cg}, weight {C8 * eight}")
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("out_dtype must be float32 or bfloat16")
+    y = torch.empty((B, Hy + KH - 1, Wy + KW - 1, Cn), dtype=out_dtype, device=g.device)
+    stream = C.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    _abi.check(_abi.load().ffmp_conv2d_dgrad_bf16(g.data_ptr(), w_bm.data_ptr(), y.data_ptr(), B, Hy, Wy, Cg, KH, KW, Cn,
+                                                  CONV_OUT_BF16 if out_dtype == torch.bfloat16 else 0, stream),
+               "ffmp_conv2d_dgrad_bf16")
+    return y
+
+
+def dgrad_bm_ok(batch: int, hy: int, wy: int, c: int, kh: int, kw: int, n: int) -> bool:
+    """Does ffmp_conv2d_dgrad_bf16 take this data gradient (c = the gradient's channels, n = the
+    input's)?  FFMP_CONV_DGRAD=ring keeps every data gradient on the padded forward kernel (A/B probe)."""
+    if os.environ.get("FFMP_CONV_DGRAD", "") == "ring":
+        return False
+    return shape_ok(2, batch, hy, wy, c, kh, kw, n)
 
 
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
@@ -143,8 +185,12 @@ class MFMAConv2dReLU(torch.autograd.Function):
         need = ctx.needs_input_grad
         gx = gw = gb = None
         if need[0]:  # the full convolution of g with the flipped, transposed kernel, on the matrix cores
-            KH = weight.shape[2]
-            gx = conv2d_nhwc(g, pack_weight_dgrad(weight), None, out_dtype=torch.bfloat16, pad=KH - 1)
+            N, Cin, KH, KW = weight.shape
+            B, Hy, Wy, _ = g.shape
+            if dgrad_bm_ok(B, Hy, Wy, N, KH, KW, Cin):  # 32 samples per MFMA block: no zero products
+                gx = conv2d_dgrad_nhwc(g, pack_weight_dgrad_bm(weight))
+            else:
+                gx = conv2d_nhwc(g, pack_weight_dgrad(weight), None, out_dtype=torch.bfloat16, pad=KH - 1)
             gx = gx.permute(0, 3, 1, 2).to(ctx.x_dtype)
         if need[1]:  # on the matrix cores too: [KH][KW][N][C] -> torch's [N][C][KH][KW]
             gw = conv2d_wgrad_nhwc(g, xb, weight.shape[2], weight.shape[3]).permute(2, 3, 0, 1).to(weight.dtype)

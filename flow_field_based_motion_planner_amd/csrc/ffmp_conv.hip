@@ -726,6 +726,171 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   return FFMP_OK;
 }
 
+// ------------------------------------------------------------------ data gradient, samples as M
+// dX[b][Y][X][n] = sum_{ky, kx, c} g[b][Y + ky - (KH-1)][X + kx - (KW-1)][c] * w'[ky][kx][n][c]: the full
+// convolution of the output gradient g (NHWC [B][Hy][Wy][C]) with the flipped, transposed kernel
+// (conv_mfma.pack_weight_dgrad).  As an implicit GEMM over output positions (conv_fwd_kernel with
+// pad = k - 1) a 32-position block spans a whole ramp of valid kernel columns and issues ~1.8x its
+// useful products at conv2's shape (a 69-wide output row, a 38-wide gradient, 32 kernel columns).
+// Here the GEMM's M is 32 SAMPLES of one output position: every row of an MFMA block has the same
+// valid taps, so a wave issues exactly the useful products — a tap (ky, kx) is skipped for the
+// whole block when its gradient cell falls outside the image (wave-uniform tests, no zero products).
+//   A = g[32 samples][16 channels of one gradient cell] (LDS), B = w'[tap][16 channels][32 n] (L1),
+//   D[sample][n] accumulates per output position, fp32.
+// A workgroup = NW waves owns one output row Y of one group of 32 samples; wave w owns the NW-strided
+// positions X = w + NW * i (i < PW), so all waves see the same share of each kernel column's valid
+// window (the parallelogram {(X, kx): 0 <= X + kx - (KW-1) < Wy}) and reach the per-phase barrier
+// together.  Phase = (ky, KQ k-steps of channels): the gradient row u = Y + ky - (KH-1), those
+// channels, every column, 32 samples — KQ KiB per column, laid out [v][k-step][h][sample][8] so a
+// fragment read is 1 KiB of consecutive bytes (ds_read_b128, conflict-free) — sits in one of two
+// LDS buffers; the next phase's row is loaded piece by piece (1 KiB per wave-instruction, a piece
+// per kernel column) into the other buffer during the sweep and published by the phase's barrier.
+// Rows are dealt heaviest first (the middle output rows meet all KH kernel rows, the border rows
+// one), so the last workgroups to start are the short ones.
+constexpr int kDgradNW = 8, kDgradPW = 9, kDgradKQ = 2;  // 72 output columns per row, 2 waves/SIMD
+
+template <int C, int N, int NW, int PW, int KQ>
+__global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16* __restrict__ g,
+                                                                 const __bf16* __restrict__ w,
+                                                                 void* __restrict__ y, int B, int Hy, int Wy,
+                                                                 int KH, int KW, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int NB = N / 32;
+  constexpr int NQ = C / (16 * KQ);  // phases per kernel row
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int G = (B + 31) / 32;
+  const int rank = blockIdx.x / G, grp = blockIdx.x % G;
+  const int padY = KH - 1, padX = KW - 1;
+  const int Hx = Hy + padY, Wx = Wy + padX;
+  const int Yc = (Hx - 1) / 2;  // rank 0, 1, 2, ... -> Yc, Yc + 1, Yc - 1, ...: most kernel rows first
+  const int Y = (rank & 1) ? Yc + (rank + 1) / 2 : Yc - rank / 2;
+  const int b0 = grp * 32;
+  const int ky_lo = max(0, padY - Y), ky_hi = min(KH - 1, padY + Hy - 1 - Y);
+  const int nph = (ky_hi - ky_lo + 1) * NQ;
+  const int colb = KQ * 1024;  // bytes of one gradient column in a buffer
+  const int bufb = Wy * colb;
+  const int npieces = Wy * KQ;
+  // this lane's sample (ragged last group: the last sample again; those rows are never stored)
+  const char* gs = (const char*)g + (size_t)min(b0 + r, B - 1) * Hy * Wy * C * 2;
+  // piece p of phase (u, q): column v = p / KQ, k-step s = p % KQ; lane (r, h) brings channels
+  // (q KQ + s) 16 + 8h .. +8 of its sample
+  auto piece = [&](int u, int q, int p) -> uint4 {
+    const int v = p / KQ, s = p - (p / KQ) * KQ;
+    return *(const uint4*)(gs + ((size_t)u * Wy + v) * C * 2 + ((q * KQ + s) * 16 + 8 * h) * 2);
+  };
+  auto piece_lds = [&](int buf, int p) -> uint4* { return (uint4*)(lds + buf * bufb + p * 1024 + lane * 16); };
+
+  {  // phase 0 into buffer 0
+    const int u0 = Y + ky_lo - padY;
+    for (int p = wave; p < npieces; p += NW) *piece_lds(0, p) = piece(u0, 0, p);
+  }
+  __syncthreads();
+
+  f32x16 acc[PW][NB];
+#pragma unroll
+  for (int i = 0; i < PW; ++i)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[i][nb] = f32x16{};
+
+  // B fragments of tap t, k-steps q KQ .. +KQ: w [KH][KW][C/8][N][8]: lane (r, h) of k-step ks reads
+  // chunk 2 ks + h, n = nb 32 + r — 1 KiB of consecutive bytes per fragment
+  auto load_b = [&](int t, int q, bf16x8 (&dst)[KQ][NB]) {
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        dst[s][nb] = *(const bf16x8*)(w + (((size_t)t * (C / 8) + 2 * (q * KQ + s) + h) * N + nb * 32 + r) * 8);
+  };
+
+  for (int ph = 0; ph < nph; ++ph) {
+    const int ky = ky_lo + ph / NQ, q = ph % NQ, buf = ph & 1;
+    const bool more = ph + 1 < nph;
+    const int u1 = Y + ky_lo + (ph + 1) / NQ - padY, q1 = (ph + 1) % NQ;
+    bf16x8 bcur[KQ][NB];
+    load_b(ky * KW, q, bcur);
+    uint4 pc = uint4{0u, 0u, 0u, 0u};
+    int pprev = -1;  // the piece held in pc, written one kernel column later
+    for (int j = 0; j < KW; ++j) {
+      bf16x8 bnx[KQ][NB];
+      load_b(ky * KW + min(j + 1, KW - 1), q, bnx);
+      if (more) {
+        if (pprev >= 0) *piece_lds(buf ^ 1, pprev) = pc;
+        const int p = wave + NW * j;
+        pprev = p < npieces ? p : -1;
+        if (pprev >= 0) pc = piece(u1, q1, p);
+      }
+      // this wave's positions whose gradient column v = X + j - padX lies in [0, Wy): i in [ilo, ihi]
+      const int t0 = padX - j - wave;
+      const int ilo = t0 <= 0 ? 0 : (t0 + NW - 1) / NW;
+      const int t1 = min(padX + Wy - 1 - j, Wx - 1) - wave;
+      const int ihi = t1 < 0 ? -1 : min(PW - 1, t1 / NW);
+      const char* abase = lds + buf * bufb + (wave + j - padX) * colb + lane * 16;
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        if (i >= ilo && i <= ihi) {
+          bf16x8 a[KQ];
+#pragma unroll
+          for (int s = 0; s < KQ; ++s) a[s] = *(const bf16x8*)(abase + NW * i * colb + s * 1024);
+#pragma unroll
+          for (int s = 0; s < KQ; ++s)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+              acc[i][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], bcur[s][nb], acc[i][nb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KQ; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) bcur[s][nb] = bnx[s][nb];
+    }
+    if (more) {
+      if (pprev >= 0) *piece_lds(buf ^ 1, pprev) = pc;
+      for (int p = wave + NW * KW; p < npieces; p += NW) *piece_lds(buf ^ 1, p) = piece(u1, q1, p);  // KW < pieces / NW
+    }
+    __syncthreads();
+  }
+
+  // epilogue: D row = sample (e & 3) + 8 (e >> 2) + 4 h, column = n (r)
+  const bool out_bf16 = flags & FFMP_CONV_OUT_BF16;
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int X = wave + NW * i;
+    if (X >= Wx) continue;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (b >= B) continue;
+        const size_t o = (((size_t)b * Hx + Y) * Wx + X) * N + nb * 32 + r;
+        if (out_bf16)
+          ((__bf16*)y)[o] = (__bf16)acc[i][nb][e];
+        else
+          ((float*)y)[o] = acc[i][nb][e];
+      }
+  }
+}
+
+template <int C, int N>
+int launch_dgrad_bm(const void* g, const void* w, void* y, int B, int Hy, int Wy, int KH, int KW, int flags,
+                    hipStream_t s) {
+  constexpr int NW = kDgradNW, PW = kDgradPW, KQ = kDgradKQ;
+  const int Hx = Hy + KH - 1, Wx = Wy + KW - 1;
+  const size_t lds = (size_t)2 * Wy * KQ * 1024;
+  if (Wx > NW * PW) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: output rows of %d > %d positions", Wx, NW * PW);
+  if (lds > 160 * 1024)
+    return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: two gradient rows of %d cells (%zu bytes) exceed the 160 KiB LDS", Wy, lds);
+  const long blocks = (long)Hx * ((B + 31) / 32);
+  if (blocks > 0x7fffffffL) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: grid too large");
+  if (t_conv_dry) return FFMP_OK;
+  hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
+                     (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d_dgrad launch: %s", hipGetErrorString(e));
+  return FFMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -768,6 +933,19 @@ int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t ba
   return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: channels in/out must be 32 or 64 (got %d / %d)", c, n);
 }
 
+int ffmp_conv2d_dgrad_bf16(const void* g, const void* w, void* dx, int32_t batch, int32_t hy, int32_t wy, int32_t c,
+                           int32_t kh, int32_t kw, int32_t n, int32_t flags, void* stream) {
+  if (!g || !w || !dx) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad_bf16: NULL tensor");
+  if (batch <= 0 || hy <= 0 || wy <= 0 || kh <= 0 || kw <= 0)
+    return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad_bf16: bad shape (batch %d, %d x %d gradient, %d x %d kernel)", batch, hy,
+                wy, kh, kw);
+  if (((uintptr_t)g | (uintptr_t)w) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad_bf16: g and w must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (c == 64 && n == 32) return launch_dgrad_bm<64, 32>(g, w, dx, batch, hy, wy, kh, kw, flags, s);
+  if (c == 32 && n == 32) return launch_dgrad_bm<32, 32>(g, w, dx, batch, hy, wy, kh, kw, flags, s);
+  return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad_bf16: gradient channels 32 or 64 and 32 output channels (got %d / %d)", c, n);
+}
+
 int ffmp_conv2d_check(int32_t kind, int32_t batch, int32_t h, int32_t wd, int32_t c, int32_t kh, int32_t kw,
                       int32_t n, int32_t pad, int32_t dx) {
   // aligned stand-in pointers: nothing is read or launched in a dry run
@@ -775,7 +953,8 @@ int ffmp_conv2d_check(int32_t kind, int32_t batch, int32_t h, int32_t wd, int32_
   t_conv_dry = true;
   const int rc = kind == 0 ? ffmp_conv2d_fwd_bf16(p, p, nullptr, p, batch, h, wd, c, kh, kw, n, pad, dx, 0, nullptr)
                : kind == 1 ? ffmp_conv2d_wgrad_bf16(p, p, static_cast<float*>(p), batch, h, wd, c, kh, kw, n, dx, 1, nullptr)
-                           : fail(FFMP_E_ARG, "ffmp_conv2d_check: kind must be 0 (forward / data gradient) or 1 (weight gradient)");
+               : kind == 2 ? ffmp_conv2d_dgrad_bf16(p, p, p, batch, h, wd, c, kh, kw, n, 0, nullptr)
+                           : fail(FFMP_E_ARG, "ffmp_conv2d_check: kind must be 0 (forward / data gradient), 1 (weight gradient) or 2 (data gradient, samples as M)");
   t_conv_dry = false;
   return rc;
 }

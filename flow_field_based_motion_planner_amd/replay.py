@@ -213,10 +213,16 @@ class ReplayMemory:
         ar = torch.arange(B, device=self.device)
         vmax = float(np.float32(self.cfg.obst_vmax))
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the compact env colours its binary16 flow planes (ffmp_bev_image compact=1): round the
+        # re-rastered float32 flow the same way (nearest even), so the learner replays exactly the
+        # images it acted on
+        compact = getattr(self.env, "obs_format", "f32") == "u8f16"
         for d in range(k):
             j = since.to(torch.int64).clamp(max=d)
             rec = recs[ar, j].contiguous()
             self._raster(rec, sm, pot if d == 0 else None, flow, newest_only=True)
+            if compact:
+                flow.copy_(flow.to(torch.float16))
             dst = out.data_ptr() + 4 * (k - 1 - d) * G2 * out.element_size()
             with torch.cuda.device(self.device):
                 _abi.check(self.lib.ffmp_bev_image(B, 0, sm[:, 1].data_ptr(), 2 * G2, flow.data_ptr(), G2, vmax, dst,

@@ -128,6 +128,14 @@ class FFMPVec:
         self.placement = None
         self.raster_shape = (0, 0)  # (cells per block, FFMP_RASTER_* flags); 0, 0 = library default
         self.raster_shape_newest = (0, 0)  # the same for newest-only launches (frame ring)
+        # the BEV image ring (bev_series) is an arena buffer like the planes: counted by the HBM
+        # budget, the auto frame window and the ring's pairing spare
+        self.bev_series = int(bev_series)
+        if self.bev_series:
+            if not self.cfg.flow:
+                raise ValueError("bev_series needs FFMPConfig(flow=True) (the flow planes it colours)")
+            if not 1 <= self.bev_series <= _abi.MAX_SERIES:
+                raise ValueError(f"bev_series must be in [1, {_abi.MAX_SERIES}]")
         self.frame_window = self._pick_window(frame_window)
         self._seamless_req = seamless if self.frame_window > 2 else False
         if seamless and self.frame_window == 2:
@@ -144,16 +152,6 @@ class FFMPVec:
         self._hist = []
         self._hist_from_reset = False
         self._alloc()
-        self.bev_series = int(bev_series)
-        self.bev = None
-        if self.bev_series:
-            if not self.cfg.flow:
-                raise ValueError("bev_series needs FFMPConfig(flow=True) (the flow planes it colours)")
-            if not 1 <= self.bev_series <= _abi.MAX_SERIES:
-                raise ValueError(f"bev_series must be in [1, {_abi.MAX_SERIES}]")
-            G = self.cfg.grid
-            self.bev = torch.zeros(self.bev_series, self.num_envs, 4, G, G, dtype=self._frame_dtype,
-                                   device=self.device)
         self._bev_pos = 0       # ring slot of the newest image
         self._bev_hist = []     # slots of the newest images, newest first (as _hist)
         self._bev_from_reset = False
@@ -249,7 +247,8 @@ class FFMPVec:
             return int(w)
         if N * G2 * 12 < self.AUTOTUNE_MIN_BYTES:  # (the f32 layout's bytes: same choice for both formats)
             return 2
-        other = N * G2 * ((self._pes if self.with_potential else 0) + (2 * self._pes if cfg.flow else 0))
+        other = N * G2 * ((self._pes if self.with_potential else 0) + (2 * self._pes if cfg.flow else 0) +
+                          4 * self.bev_series * self._fes)
         free, _ = torch.cuda.mem_get_info(self.device)
         free += max(0, int(self.lib.ffmp_ring_pool_bytes(self.device.index)))  # parked pieces are reused
         room = self.WINDOW_HBM_FRACTION * free - other
@@ -280,6 +279,8 @@ class FFMPVec:
             ("truncated", (N,), b),
             # optional: post-step state before auto-reset (ffmp_state_t.term_*)
             ("term_record", (N, cfg.record_len()), f32), ("term_obs", (N, 5), f32),
+            # optional: the last bev_series 4-channel BEV images of every env (ffmp_bev_image)
+            ("bev", (max(getattr(self, "bev_series", 0), 1), N, 4, G, G), self._frame_dtype),
         ]
         if not self.with_potential:
             specs = [sp for sp in specs if sp[0] != "potential"]
@@ -289,6 +290,8 @@ class FFMPVec:
             specs = [sp for sp in specs if sp[0] != "lidar"]
         if not self.keep_terminal:
             specs = [sp for sp in specs if not sp[0].startswith("term_")]
+        if not getattr(self, "bev_series", 0):
+            specs = [sp for sp in specs if sp[0] != "bev"]
         if not with_frames:
             specs = [sp for sp in specs if sp[0] != "frames"]
         return specs
@@ -362,6 +365,7 @@ class FFMPVec:
         self.flow = None
         self.term_record = None
         self.term_obs = None
+        self.bev = None
         if self.arena:
             self._arena_offs, off = [], 0
             for _, shape, dtype in specs:
@@ -1376,7 +1380,7 @@ class FFMPVec:
         if self.ring == "seamless" and getattr(self, "_ring", None) is not None:
             ring = self.frame_window * self._ring.slot_stride
         if self._arena_buf is not None:
-            return self._arena_buf.numel() + ring + (self.bev.numel() * self.bev.element_size() if self.bev is not None else 0)
+            return self._arena_buf.numel() + ring  # the BEV ring included (an arena buffer)
         return ring + sum(t.numel() * t.element_size() for t in vars(self).values()
                           if isinstance(t, torch.Tensor) and not (ring and t is self.frames))
 

@@ -319,8 +319,21 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
 int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t batch, int32_t h, int32_t wd, int32_t c,
                            int32_t kh, int32_t kw, int32_t n, int32_t dx, int32_t chunks, void* stream);
 
-/* Would ffmp_conv2d_fwd_bf16 (kind 0; with pad > 0 the data-gradient form) or
- * ffmp_conv2d_wgrad_bf16 (kind 1; pad ignored) accept this shape?  Runs every check of the launch
+/* The data gradient of the same convolutions with the batch as the GEMM's M (the backward of
+ * src/train.py:235's conv2 through autograd, :426-428):
+ *   dx[b][Y][X][n] = sum_{ky,kx,c} g[b][Y+ky-(kh-1)][X+kx-(kw-1)][c] * w[ky][kx][c/8][n][c%8]
+ * (cells outside g are zero: the full convolution).  g NHWC bf16 [batch][hy][wy][c] (the output
+ * gradient); w bf16 [kh][kw][c/8][n][8] = the flipped, transposed kernel w'[ky][kx][n][c] =
+ * w[n'=c][c'=n][kh-1-ky][kw-1-kx] with its channels in 8-blocks ahead of n; dx NHWC
+ * [batch][hy+kh-1][wy+kw-1][n], fp32 or (FFMP_CONV_OUT_BF16) bf16.  32 samples share each MFMA
+ * block, so every issued product is a useful one.  c = 32 or 64, n = 32; output rows of <= 72
+ * positions; two gradient rows of KQ = 2 k-steps in LDS (wy <= 40). */
+int ffmp_conv2d_dgrad_bf16(const void* g, const void* w, void* dx, int32_t batch, int32_t hy, int32_t wy, int32_t c,
+                           int32_t kh, int32_t kw, int32_t n, int32_t flags, void* stream);
+
+/* Would ffmp_conv2d_fwd_bf16 (kind 0; with pad > 0 the data-gradient form),
+ * ffmp_conv2d_wgrad_bf16 (kind 1; pad ignored) or ffmp_conv2d_dgrad_bf16 (kind 2: h, wd = the
+ * gradient's hy, wy; pad, dx ignored) accept this shape?  Runs every check of the launch
  * (channels, batch <= 65535, 16 KiB input rows, the LDS ring / stage, wgrad rows of >= 8
  * positions) and launches nothing.  FFMP_OK, or FFMP_E_ARG with the reason in ffmp_last_error().
  * The learner asks before it routes a convolution to the matrix-core kernels, and keeps the

@@ -125,25 +125,27 @@ def test_bev_maps_errors_and_reload():
         env.bev_maps(2, out=torch.empty(8, 4, 64, 64, device=DEV))
 
 
-def test_replay_bev_series_reproduces_the_env():
+@pytest.mark.parametrize("obs_format", ["f32", "u8f16"])
+def test_replay_bev_series_reproduces_the_env(obs_format):
     """ReplayMemory(series=3, bev=True): the state series re-rastered and coloured from the stored
     records equals env.bev_maps(3) before the step; the observation series equals it after the step,
-    or for an env that reset, the state series slid by one with the terminal image appended."""
+    or for an env that reset, the state series slid by one with the terminal image appended.  In the
+    compact layout the env colours binary16 flow planes, and so must the replay."""
     cfg = FFMPConfig(grid=64, n_obst=12, n_beams=32, moving=True, max_steps=5, obst_rmax=0.5, obst_vmax=1.2,
                      world_half=2.4, goal_min=0.6, goal_max=1.5, flow=True, seed=23)
     N, T, k = 32, 11, 3
-    env = FFMPVec(N, cfg, device=DEV, keep_terminal=True, bev_series=k)
+    env = FFMPVec(N, cfg, device=DEV, keep_terminal=True, bev_series=k, obs_format=obs_format)
     mem = ReplayMemory(env, capacity=N * T, series=k, bev=True)
     env.reset()
     rng = np.random.default_rng(2)
     before, after, term, dones = [], [], [], []
     for _ in range(T):
-        before.append(env.bev_maps(k).clone())
+        before.append(env.bev_maps(k).float())
         mem.push_begin()
         a = torch.as_tensor(rng.integers(0, 28, N), device=DEV)
         env.step(a)
         mem.push_end(a)
-        after.append(env.bev_maps(k).clone())
+        after.append(env.bev_maps(k).float())
         term.append(env.term_record.clone())
         dones.append(env.done.clone())
     done_all = torch.cat(dones)
@@ -157,6 +159,8 @@ def test_replay_bev_series_reproduces_the_env():
     assert torch.equal(tr.observe_m[done_all][:, :-4], s_want[done_all][:, 4:])
     oc = Cfg.from_config(cfg)
     sm, _, flow = raster(oc, Record.unpack(torch.cat(term)[done_all].cpu().numpy(), cfg.n_obst), False)
+    if obs_format == "u8f16":
+        flow = flow.astype(np.float16).astype(np.float32)
     newest = bev_image(sm[:, 1], flow, cfg.obst_vmax)
     assert np.array_equal(tr.observe_m[done_all][:, -4:].cpu().numpy(), newest)
     mem2 = ReplayMemory(env, capacity=N * T, series=k, bev=True)
@@ -189,3 +193,22 @@ def test_brain_twelve_channels_updates(amp):
     assert losses and all(np.isfinite(losses))
     with pytest.raises(ValueError, match="bev_series"):
         Brain(FFMPVec(n, cfg, device=DEV, keep_terminal=True, autotune=False), input_channels=12)
+
+
+def test_bev_ring_counts_against_the_hbm_budget():
+    """the BEV image ring is an arena buffer — a budget that holds the planes but not the
+    ring is refused at construction, and an instance built within a budget holds the ring inside it."""
+    cfg = FFMPConfig(grid=64, n_obst=4, n_beams=0, moving=True, max_steps=20, flow=True, seed=3)
+    N, k = 4096, 3
+    ring = k * N * 4 * 64 * 64 * 4  # 768 MiB
+    planes = N * 64 * 64 * 4 * (2 + 1 + 2)  # frames (W = 2), potential, flow: 320 MiB
+    with pytest.raises(ValueError):
+        FFMPVec(N, cfg, device=DEV, bev_series=k, hbm_budget=planes + ring // 2, autotune=False)
+    env = FFMPVec(N, cfg, device=DEV, bev_series=k, hbm_budget=planes + ring + (64 << 20), autotune=False)
+    assert env.hbm_bytes() <= planes + ring + (64 << 20)
+    a0 = env._arena_buf.data_ptr()
+    assert a0 <= env.bev.data_ptr() < a0 + env._arena_buf.numel()
+    env.reset()
+    env.step(torch.zeros(N, dtype=torch.int64, device=DEV))
+    assert env.bev_maps(k).shape == (N, 4 * k, 64, 64)
+    env.close()

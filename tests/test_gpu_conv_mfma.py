@@ -61,9 +61,10 @@ def test_conv_fwd_matches_float64(B, H, W, C, K, N, pad):
                                        (3, 64, 31, 64, 8), (2, 64, 24, 64, 8), (3, 64, 17, 64, 8)])  # conv4 x 3
 def test_autograd_function_against_autocast_and_float64(B, C, H, N, K):
     """relu(conv) of the reference Network's conv2 / conv3 / conv4 shapes: the forward within bf16
-    rounding of autocast's conv2d; the gradients (input: the MFMA kernel's full convolution;
-    weight / bias: MIOpen bf16 on the saved operands; all masked by the kernel's own output) against
-    float64 autograd of the same masked product."""
+    rounding of autocast's conv2d; the gradients (input: the MFMA data-gradient kernel — samples as M
+    where ffmp_conv2d_dgrad_bf16 takes the shape, else the padded full convolution; weight: the MFMA
+    weight-gradient kernel; bias: an fp32 sum; all masked by the kernel's own output) against float64
+    autograd of the same masked product."""
     g = torch.Generator(device=DEV).manual_seed(7 + H)
     conv = torch.nn.Conv2d(C, N, kernel_size=K).to(DEV)
     x = torch.relu(torch.randn((B, C, H, H), device=DEV, generator=g)).to(torch.bfloat16).requires_grad_(True)
@@ -184,3 +185,44 @@ def test_wgrad_matches_float64(B, H, W, C, KH, KW, N, dx):
     err = (dw.double() - ref).abs()
     bad = err > 5e-5 * absref + 1e-6
     assert not bool(bad.any()), f"{int(bad.sum())} of {bad.numel()} outside tolerance, max err {float(err.max())}"
+
+
+@pytest.mark.parametrize("B,Hy,Wy,C,KH,KW,N", [
+    (2, 38, 38, 64, 32, 32, 32),    # conv2's data gradient (the reference Network, train.py:235)
+    (33, 38, 38, 64, 32, 32, 32),   # a ragged second sample group (one sample)
+    (64, 38, 38, 64, 32, 32, 32),   # two full groups
+    (3, 38, 38, 32, 32, 32, 32),    # 32 gradient channels: one phase per kernel row
+    (5, 20, 24, 64, 5, 7, 32),      # a small kernel: pieces left after the kernel-column sweep
+    (2, 7, 40, 64, 3, 33, 32),      # the widest gradient rows (LDS) and output rows of 72 positions
+    (4, 1, 1, 32, 2, 3, 32)])       # a single gradient cell
+def test_dgrad_samples_as_m_matches_float64(B, Hy, Wy, C, KH, KW, N):
+    """ffmp_conv2d_dgrad_bf16 (32 samples per MFMA block, every tap of every position exact) against
+    torch's float64 input gradient of the same bf16 operands (torch.nn.grad.conv2d_input); the
+    forward's tolerance.  The bf16 output is the fp32 result rounded."""
+    from flow_field_based_motion_planner_amd.conv_mfma import conv2d_dgrad_nhwc, dgrad_bm_ok, pack_weight_dgrad_bm
+    assert dgrad_bm_ok(B, Hy, Wy, C, KH, KW, N)
+    g0 = torch.Generator(device=DEV).manual_seed(B + Hy + KW + C)
+    g = torch.randn((B, Hy, Wy, C), device=DEV, generator=g0).to(torch.bfloat16)
+    w = torch.randn((C, N, KH, KW), device=DEV, generator=g0) / (C * KH * KW) ** 0.5  # forward: N -> C channels
+    wb = pack_weight_dgrad_bm(w)
+    dx = conv2d_dgrad_nhwc(g, wb, out_dtype=torch.float32)
+    Hx, Wx = Hy + KH - 1, Wy + KW - 1
+    assert dx.shape == (B, Hx, Wx, N)
+    g64, w64 = g.double().permute(0, 3, 1, 2), w.to(torch.bfloat16).double()
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = torch.nn.grad.conv2d_input((B, N, Hx, Wx), w64, g64).permute(0, 2, 3, 1)
+        absref = torch.nn.grad.conv2d_input((B, N, Hx, Wx), w64.abs(), g64.abs()).permute(0, 2, 3, 1)
+    err = (dx.double() - ref).abs()
+    bad = err > 5e-5 * absref + 1e-6
+    assert not bool(bad.any()), f"{int(bad.sum())} of {bad.numel()} outside tolerance, max err {float(err.max())}"
+    assert torch.equal(conv2d_dgrad_nhwc(g, wb), dx.to(torch.bfloat16))
+
+
+def test_dgrad_samples_as_m_shape_limits():
+    """The launch's own checks (ffmp_conv2d_check kind 2): 32-channel outputs only, output rows of at
+    most 72 positions, two gradient rows within the LDS."""
+    from flow_field_based_motion_planner_amd.conv_mfma import dgrad_bm_ok
+    assert dgrad_bm_ok(256, 38, 38, 64, 32, 32, 32) and dgrad_bm_ok(1024, 38, 38, 64, 32, 32, 32)
+    assert not dgrad_bm_ok(256, 31, 31, 64, 8, 8, 64)   # conv3's: 64 output channels
+    assert not dgrad_bm_ok(2, 5, 10, 64, 3, 64, 32)     # output rows of 73 positions
+    assert not dgrad_bm_ok(2, 10, 41, 64, 3, 3, 32)     # 41 columns x 2 KiB x 2 rows > 160 KiB

@@ -170,10 +170,12 @@ def test_bench_traffic_lookup():
         if not os.path.exists(path):
             continue
         d = json.load(open(path))
-        got = bench.load_traffic(name, d["n_envs"], d["frame_window"], d["ring"], fused, fmt)
+        got, src = bench.load_traffic(name, d["n_envs"], d["frame_window"], d["ring"], fused, fmt)
         assert got == d["raster_hbm_bytes_per_launch"]
-        assert bench.load_traffic(name, d["n_envs"] + 1, d["frame_window"], d["ring"], fused, fmt) is None
-        assert bench.load_traffic(name, d["n_envs"], d["frame_window"] + 1, d["ring"], fused, fmt) is None
+        # the line names the profile the figure came from (roofline.traffic_source)
+        assert os.path.samefile(os.path.join(prof, "..", src), path)
+        assert bench.load_traffic(name, d["n_envs"] + 1, d["frame_window"], d["ring"], fused, fmt) == (None, None)
+        assert bench.load_traffic(name, d["n_envs"], d["frame_window"] + 1, d["ring"], fused, fmt) == (None, None)
     assert bench.load_traffic("C3", 32768, 8, "seamless", False, "u8f16") != bench.load_traffic("C3", 32768, 8,
                                                                                                "seamless", False)
 

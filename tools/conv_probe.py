@@ -9,8 +9,9 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from flow_field_based_motion_planner_amd.conv_mfma import (conv2d_nhwc, conv2d_wgrad_nhwc, fold_input,  # noqa: E402
-                                                          pack_weight, pack_weight_dgrad, pack_weight_fold)
+from flow_field_based_motion_planner_amd.conv_mfma import (conv2d_dgrad_nhwc, conv2d_nhwc, conv2d_wgrad_nhwc,  # noqa: E402
+                                                          fold_input, pack_weight, pack_weight_dgrad,
+                                                          pack_weight_dgrad_bm, pack_weight_fold)
 
 dev = torch.device("cuda:0")
 torch.backends.cudnn.benchmark = True
@@ -48,6 +49,8 @@ for B in [int(a) for a in ([a for a in sys.argv[1:] if not a.startswith("--")] o
     gn = gy.permute(0, 2, 3, 1).contiguous()
     wd = pack_weight_dgrad(w)
     rows["mfma dgrad (pad 31, bf16 out)"] = timeit(lambda: conv2d_nhwc(gn, wd, None, out_dtype=torch.bfloat16, pad=31))
+    wbm = pack_weight_dgrad_bm(w)
+    rows["mfma dgrad bm (bf16 out)"] = timeit(lambda: conv2d_dgrad_nhwc(gn, wbm))
     if not MFMA_ONLY:
         rows["miopen dgrad NCHW"] = timeit(lambda: torch.ops.aten.convolution_backward(
             gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False]))

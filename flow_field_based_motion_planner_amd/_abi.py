@@ -116,6 +116,7 @@ _SIGS = {
     "ffmp_conv2d_fwd_bf16": (C.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32,
                                        _P]),
     "ffmp_conv2d_wgrad_bf16": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    "ffmp_reward_done_packed": (C.c_int, [C.POINTER(CfgT), _P, _P, _I64, _I32, _I64, _I32, _I32, _P]),
     "ffmp_conv2d_dgrad_bf16": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
     "ffmp_conv2d_check": (C.c_int, [_I32] * 10),
     "ffmp_episode_init": (C.c_int, [_I64, _P, _I32, C.POINTER(EpisodeT), _P]),

@@ -1347,27 +1347,48 @@ static int check_episode(const ffmp_episode_t* ep) {
   return FFMP_OK;
 }
 
+// LDS a block may use on this device (static + dynamic), read once
+size_t device_lds_limit() {
+  static const size_t lim = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0)
+      return (size_t)64 * 1024;
+    return (size_t)v;
+  }();
+  return lim;
+}
+
+// false (nothing launched) when the block's LDS — the static disc / footprint arrays, which grow
+// with the discs per lane, plus trace_discs' dynamic beam minima (W x envs per wave x L words) —
+// exceeds what a block may use: the caller then tries a layout that needs less
 template <int MODE, int W, int LPE, int DPL>
-void launch_env_t(const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action, const uint8_t* mask,
+bool launch_env_t(const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action, const uint8_t* mask,
                   int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob, const ffmp_out_t& o,
                   hipStream_t s) {
+  static const size_t static_lds = [] {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&env_kernel<MODE, W, LPE, DPL>)) == hipSuccess
+               ? (size_t)a.sharedSizeBytes
+               : (size_t)0;
+  }();
   const int64_t per_block = (int64_t)W * (64 / LPE);
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const size_t lds = (size_t)W * (64 / LPE) * (size_t)cfg.n_beams * sizeof(uint32_t);  // trace_discs' beam minima
+  if (static_lds + lds > device_lds_limit()) return false;
   hipLaunchKernelGGL((env_kernel<MODE, W, LPE, DPL>), dim3(blocks), dim3(64 * W), lds, s, cfg, n, env_offset, action,
                      mask, initial, st, ob, o);
+  return true;
 }
 
-// (lanes per env, discs per lane) pairs with an env_kernel instance; false if there is none
+// (lanes per env, discs per lane) pairs with an env_kernel instance; false if there is none or its
+// block would not fit the LDS
 template <int MODE, int W>
 bool launch_env_mode(int lpe, int dpl, const ffmp_cfg_t& cfg, int64_t n, int64_t env_offset, const int64_t* action,
                      const uint8_t* mask, int32_t initial, const ffmp_state_t& st, const ffmp_obs_t& ob,
                      const ffmp_out_t& o, hipStream_t s) {
 #define FFMP_ENV_CASE(L_, D_)                                                                    \
-  if (lpe == L_ && dpl == D_) {                                                                  \
-    launch_env_t<MODE, W, L_, D_>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);      \
-    return true;                                                                                 \
-  }
+  if (lpe == L_ && dpl == D_) return launch_env_t<MODE, W, L_, D_>(cfg, n, env_offset, action, mask, initial, st, ob, o, s);
   FFMP_ENV_CASE(16, 1) FFMP_ENV_CASE(32, 1) FFMP_ENV_CASE(64, 1) FFMP_ENV_CASE(8, 2) FFMP_ENV_CASE(16, 2)
   FFMP_ENV_CASE(4, 4) FFMP_ENV_CASE(8, 1)
 #undef FFMP_ENV_CASE
@@ -1647,14 +1668,18 @@ static int launch_env(int mode, const ffmp_cfg_t* cfg, int64_t n, int64_t env_of
   int dpl = cfg->n_obst <= lpe ? 1 : (cfg->n_obst + lpe - 1) / lpe;
   const hipStream_t hs = (hipStream_t)stream;
   const bool w4 = tu.env_waves == 4;
-  bool ok = w4 ? launch_env_lpe<4>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs)
-               : launch_env_lpe<1>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs);
-  if (!ok) {
-    lpe = need;
-    dpl = 1;
-    ok = w4 ? launch_env_lpe<4>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs)
-            : launch_env_lpe<1>(mode, lpe, dpl, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs);
-  }
+  auto try_launch = [&](bool four, int l, int d) {
+    return four ? launch_env_lpe<4>(mode, l, d, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs)
+                : launch_env_lpe<1>(mode, l, d, *cfg, n, env_offset, action, mask, initial, *state, *obs, o, hs);
+  };
+  // the tuned layout; one wave per block (a quarter of the LDS); one disc per lane on the fewest
+  // lanes that hold the discs (the smallest static arrays) — the last always fits (64 lanes x 1
+  // disc x 72 B + one env's L <= 1024 words)
+  const bool ok = try_launch(w4, lpe, dpl) || (w4 && try_launch(false, lpe, dpl)) ||
+                  (w4 && try_launch(true, need, 1)) || try_launch(false, need, 1);
+  if (!ok)
+    return fail(FFMP_E_ARG, "no env_kernel layout fits the %zu B of LDS a block may use (K = %d, L = %d)",
+                device_lds_limit(), cfg->n_obst, cfg->n_beams);
   return check_launch(mode == kEnvMode_Step ? "ffmp_step_state" : "ffmp_reset");
 }
 
@@ -1806,6 +1831,34 @@ int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n, const double* scan, int32
                      scan_len, local_map, map_stride, collide_in, goal_in, rel_goal, is_first, d0, reward,
                      done, is_goal, collide);
   return check_launch("ffmp_reward_done");
+}
+
+int ffmp_reward_done_packed(const ffmp_cfg_t* cfg, void* host_buf, void* dev_buf, int64_t in_bytes, int32_t scan_len,
+                            int64_t map_off, int32_t map_grid, int32_t flags, void* stream) {
+  if (!host_buf || !dev_buf) return fail(FFMP_E_ARG, "ffmp_reward_done_packed: NULL buffer");
+  if (scan_len < 0 || in_bytes < 48 + 8 * (int64_t)scan_len)
+    return fail(FFMP_E_ARG, "ffmp_reward_done_packed: %lld bytes cannot hold %d beams", (long long)in_bytes, scan_len);
+  const bool with_map = flags & 4;
+  if (with_map && (map_grid <= 0 || map_off < 48 + 8 * (int64_t)scan_len || map_off % 16 ||
+                   map_off + 4 * (int64_t)map_grid * map_grid > in_bytes))
+    return fail(FFMP_E_ARG, "ffmp_reward_done_packed: map of %d^2 at byte %lld outside the %lld-byte buffer", map_grid,
+                (long long)map_off, (long long)in_bytes);
+  if (((uintptr_t)host_buf | (uintptr_t)dev_buf) & 15) return fail(FFMP_E_ARG, "ffmp_reward_done_packed: buffers must be 16-byte aligned");
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(dev_buf, host_buf, (size_t)in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail(FFMP_E_HIP, "ffmp_reward_done_packed: host -> device copy failed");
+  char* d = (char*)dev_buf;
+  uint8_t* u = (uint8_t*)dev_buf;
+  const int rc = ffmp_reward_done(cfg, 1, scan_len ? (const double*)(d + 48) : nullptr, scan_len,
+                                  with_map ? (const float*)(d + map_off) : nullptr, (int64_t)map_grid * map_grid,
+                                  (flags & 1) ? u + 41 : nullptr, (flags & 2) ? u + 42 : nullptr, (const double*)(d + 24),
+                                  u + 40, (double*)(d + 8), (double*)d, u + 16, u + 17, u + 18, stream);
+  if (rc) return rc;
+  if (hipMemcpyAsync(host_buf, dev_buf, 24, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(FFMP_E_HIP, "ffmp_reward_done_packed: device -> host copy failed");
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_reward_done_packed: %s", hipGetErrorString(e));
+  return FFMP_OK;
 }
 
 int ffmp_footprint_collision(const ffmp_cfg_t* cfg, int64_t n, const float* local_map, int64_t map_stride,

@@ -5,8 +5,8 @@ Mirrors src/gym_ffmp/envs/ffmp.py:22-188 of the reference
 
   attributes / spaces         ffmp.py:25-64  (action Box [0,-.6]..[.6,.6]; obs Dict
                               local_map int32 (G,G,1), relative_goal, velocity)
-  is_collision(local_map)     ffmp.py:85-105  -> ffmp_footprint_collision kernel
-  is_collision2(scan_data)    ffmp.py:108-117 -> ffmp_scan_collision_f64 kernel (+ the
+  is_collision(local_map)     ffmp.py:85-105  -> the footprint test of ffmp_reward_done
+  is_collision2(scan_data)    ffmp.py:108-117 -> the lidar test of ffmp_reward_done (+ the
                               reference's "!!!..." banner on a hit, unless verbose=False)
   is_goal(d)                  ffmp.py:120-127 -> ffmp_reward_done kernel
   reward_calculator(...)      ffmp.py:130-157 -> ffmp_reward_done kernel; keeps the
@@ -14,6 +14,9 @@ Mirrors src/gym_ffmp/envs/ffmp.py:22-188 of the reference
                               every FFMP instance, NameError before the first is_first)
   is_done(col, goal)          ffmp.py:160-164 (host boolean)
   rewarder / rewarder2        ffmp.py:167-188 -> one ffmp_reward_done launch each
+Each of these is ONE library call (ffmp_reward_done_packed): the inputs packed into a pinned host
+buffer, one copy in, the kernel, one copy out, the stream synchronized; the footprint is cached per
+(map attributes, width) instead of rebuilt over all G^2 cells per call (ffmp.py:87-94).
 
 New (the reference's reset is commented out, ffmp.py:77-83, and it has no step):
   reset(seed=None) -> obs,  step(action_id) -> (obs, reward, done, info)  [gym 0.17/0.18
@@ -93,6 +96,8 @@ class FFMP(GymEnvBase):
         self.robot_grids = []
         self._vec = None
         self._needs_reset = True
+        self._cfg_cache = {}  # (map attributes, width) -> (ctypes cfg with the footprint, robot_grids)
+        self._stage = None    # pinned host / device staging buffers of the legacy methods
 
     # ------------------------------------------------------------- plumbing
     @property
@@ -106,7 +111,14 @@ class FFMP(GymEnvBase):
     def _legacy_cfg(self, grid: int):
         """ctypes cfg for the legacy kernels: the footprint of THIS instance's map
         attributes (ffmp.py:87-94 reads self.map_grid_num / map_grid_size / map_range
-        / robot_rsize) as absolute cells, re-centred on the given map's width."""
+        / robot_rsize) as absolute cells, re-centred on the given map's width.  The reference
+        rebuilds the footprint over all G^2 cells on every call; here it is built once per
+        (attributes, map width) and cached (the attributes are public and may be changed)."""
+        key = (grid, self.map_grid_num, self.map_grid_size, self.map_range, self.robot_rsize, id(self.cfg))
+        hit = self._cfg_cache.get(key)
+        if hit is not None and hit[2] is self.cfg:  # (a config is replaced, never mutated: FFMPConfig.replace)
+            self.robot_grids = hit[1]
+            return hit[0]
         if grid % 4 or grid < 8:
             raise ValueError(f"local map width must be a multiple of 4 and >= 8, got {grid}")
         cells = []
@@ -125,20 +137,35 @@ class FFMP(GymEnvBase):
         c.n_foot = len(cells)
         for k, (i, j) in enumerate(cells):
             c.foot_di[k], c.foot_dj[k] = i - grid // 2, j - grid // 2
-        c.robot_r = float(self.robot_rsize)
+        # the lidar threshold: is_collision2 compares with the module constant ROBOT_RSIZE
+        # (ffmp.py:112), not with self.robot_rsize (which only shapes the footprint above)
+        c.robot_r = float(ROBOT_RSIZE)
+        if len(self._cfg_cache) >= 64:
+            self._cfg_cache.clear()
+        self._cfg_cache[key] = (c, self.robot_grids, self.cfg)
         return c
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    # One call of the legacy surface = one host->device copy of every input packed into a pinned
+    # staging buffer, one ffmp_reward_done launch, one device->host copy of every output, all in one
+    # library call (include/ffmp.h ffmp_reward_done_packed).  Packed layout (bytes): outputs reward f64 @0, d0 f64 @8 (in/out), done / is_goal /
+    # collide u8 @16..18; inputs rel_goal f64[2] @24, is_first / collide_in / goal_in u8 @40..42,
+    # scan f64[L] @48, the local map f32[G*G] after it (16-aligned).
+    def _staging(self, nbytes: int):
+        st = self._stage
+        if st is None or st[0].numel() < nbytes:
+            cap = max(4096, 1 << (int(nbytes) - 1).bit_length())
+            hin = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            st = self._stage = (hin, torch.empty(cap, dtype=torch.uint8, device=self.device), hin.numpy())
+        return st
+
     def _reward_done(self, rel_goal, is_first: bool, d0: float, scan=None, local_map=None,
                      collide_in=None, goal_in=None):
         lib = _abi.load()
-        dev = self.device
-        f64 = dict(dtype=torch.float64, device=dev)
-        u8 = dict(dtype=torch.uint8, device=dev)
         grid = self.cfg.grid
-        m_t = None
+        m = None
         if local_map is not None:
             m = np.asarray(local_map)
             if m.ndim == 3:
@@ -146,53 +173,43 @@ class FFMP(GymEnvBase):
             if m.ndim != 2 or m.shape[0] != m.shape[1]:
                 raise ValueError(f"local_map must be (G,G) or (G,G,1), got {np.shape(local_map)}")
             grid = m.shape[0]
-            m_t = torch.as_tensor(np.ascontiguousarray(m, dtype=np.float32)).to(dev)
         cfg_c = self._legacy_cfg(grid)
-        s_t = None
-        L = 0
-        if scan is not None:
-            vals = np.array([0.0 if v is None else float(v) for v in scan], dtype=np.float64)
-            L = len(vals)
-            s_t = torch.as_tensor(vals).to(dev) if L else None
-        rg = torch.tensor([float(rel_goal[0]), float(rel_goal[1]) if len(rel_goal) > 1 else 0.0], **f64)
-        first = torch.tensor([1 if is_first else 0], **u8)
-        d0_t = torch.tensor([d0], **f64)
-        ci = None if collide_in is None else torch.tensor([1 if collide_in else 0], **u8)
-        gi = None if goal_in is None else torch.tensor([1 if goal_in else 0], **u8)
-        reward = torch.empty(1, **f64)
-        done, goal, col = (torch.empty(1, **u8) for _ in range(3))
-        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-        _abi.check(lib.ffmp_reward_done(C.byref(cfg_c), 1, p(s_t), L, p(m_t), grid * grid, p(ci), p(gi),
-                                        rg.data_ptr(), first.data_ptr(), d0_t.data_ptr(), reward.data_ptr(),
-                                        done.data_ptr(), goal.data_ptr(), col.data_ptr(), self._stream()),
-                   "ffmp_reward_done")
-        out = torch.cat([reward, d0_t, done.double(), goal.double(), col.double()]).cpu().numpy()
-        return float(out[0]), float(out[1]), bool(out[2]), bool(out[3]), bool(out[4])
+        # the scan as float64: None (the reference's list head, src/train.py:97) -> NaN, which like
+        # None and 0.0 never counts as a hit (`bool(r) and r < 0.13`, ffmp.py:112: NaN < 0.13 is false)
+        vals = None if scan is None else np.asarray(scan, dtype=np.float64).reshape(-1)
+        L = 0 if vals is None else vals.size
+        moff = -(-(48 + 8 * L) // 16) * 16
+        nbytes = moff + (0 if m is None else 4 * grid * grid)
+        hin, din, hnp = self._staging(nbytes)
+        hnp[8:16].view(np.float64)[0] = d0
+        hnp[24:40].view(np.float64)[:] = (float(rel_goal[0]), float(rel_goal[1]) if len(rel_goal) > 1 else 0.0)
+        hnp[40:43] = (1 if is_first else 0, 1 if collide_in else 0, 1 if goal_in else 0)
+        if L:
+            hnp[48:48 + 8 * L].view(np.float64)[:] = vals
+        if m is not None:
+            hnp[moff:nbytes].view(np.float32).reshape(grid, grid)[:] = m
+        flags = (0 if collide_in is None else 1) | (0 if goal_in is None else 2) | (0 if m is None else 4)
+        # one library call: the copy in, the kernel, the copy out, the stream synchronized
+        _abi.check(lib.ffmp_reward_done_packed(C.byref(cfg_c), hin.data_ptr(), din.data_ptr(), nbytes, L, moff, grid,
+                                               flags, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "ffmp_reward_done_packed")
+        r, d0n = hnp[0:16].view(np.float64)
+        return float(r), float(d0n), bool(hnp[16]), bool(hnp[17]), bool(hnp[18])
 
     # ---------------------------------------------------- reference methods
     def is_collision(self, local_map_info) -> bool:
         m = np.asarray(local_map_info)
         if m.ndim == 3:
             m = m[:, :, 0]
-        grid = m.shape[0]
-        cfg_c = self._legacy_cfg(grid)
-        dev = self.device
-        m_t = torch.as_tensor(np.ascontiguousarray(m, dtype=np.float32)).to(dev)
-        col = torch.empty(1, dtype=torch.uint8, device=dev)
-        _abi.check(_abi.load().ffmp_footprint_collision(C.byref(cfg_c), 1, m_t.data_ptr(), grid * grid,
-                                                        col.data_ptr(), self._stream()), "ffmp_footprint_collision")
-        return bool(col.item())
+        # the footprint test alone: one packed ffmp_reward_done call with the map and no scan
+        return self._reward_done((1.0, 0.0), True, 0.0, local_map=m)[4]
 
     def is_collision2(self, scan_data) -> bool:
-        vals = np.array([0.0 if v is None else float(v) for v in scan_data], dtype=np.float64)
+        vals = np.asarray(scan_data, dtype=np.float64).reshape(-1)  # None -> NaN: never a hit, as None
         if len(vals) == 0:
             return False
-        dev = self.device
-        s_t = torch.as_tensor(vals).to(dev)
-        col = torch.empty(1, dtype=torch.uint8, device=dev)
-        _abi.check(_abi.load().ffmp_scan_collision_f64(1, len(vals), s_t.data_ptr(), float(ROBOT_RSIZE),
-                                                       col.data_ptr(), None, self._stream()), "ffmp_scan_collision")
-        hit = bool(col.item())
+        # the lidar test alone (threshold ROBOT_RSIZE): one packed ffmp_reward_done call, no map
+        hit = self._reward_done((1.0, 0.0), True, 0.0, scan=vals)[4]
         if hit and self.verbose:
             print(_BANNER)
         return hit

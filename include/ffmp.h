@@ -274,6 +274,19 @@ int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n,
                      double* reward, uint8_t* done, uint8_t* is_goal, uint8_t* collide,
                      void* stream);
 
+/* One call of the single-env surface — FFMP.rewarder / rewarder2 / reward_calculator / is_goal
+ * (src/gym_ffmp/envs/ffmp.py:120-188; rewarder2 is the one env call src/train.py:577 makes per
+ * step) — from one packed buffer: host_buf (pinned host memory, 16-byte aligned) -> dev_buf (device,
+ * >= in_bytes) in one copy, one ffmp_reward_done launch (n = 1), the 24 output bytes back into
+ * host_buf in one copy, then the stream is synchronized: the results are in host_buf on return.
+ * Layout (bytes): outputs reward f64 @0, d0 f64 @8 (in: the episode-start distance, out: set on
+ * is_first), done / is_goal / collide u8 @16, 17, 18; inputs rel_goal f64[2] @24, is_first /
+ * collide_in / goal_in u8 @40, 41, 42, scan f64[scan_len] @48, the local map f32[map_grid^2] @map_off
+ * (16-aligned, >= 48 + 8 scan_len).  flags: 1 = collide_in given, 2 = goal_in given, 4 = a local map
+ * (cfg's footprint; cfg->grid need not equal map_grid). */
+int ffmp_reward_done_packed(const ffmp_cfg_t* cfg, void* host_buf, void* dev_buf, int64_t in_bytes, int32_t scan_len,
+                            int64_t map_off, int32_t map_grid, int32_t flags, void* stream);
+
 /* FFMP.is_collision: any local_map[(G/2+di), (G/2+dj)] > 0 over the footprint. */
 int ffmp_footprint_collision(const ffmp_cfg_t* cfg, int64_t n, const float* local_map,
                              int64_t map_stride, uint8_t* collide, void* stream);

@@ -262,3 +262,17 @@ def test_closed_env_refuses_every_launch():
                  lambda: v._step_fused(act), lambda: v.load_state_dict(sd), lambda: v.state_dict()):
         with pytest.raises(RuntimeError, match="closed"):
             call()
+
+
+def test_footprint_cache_follows_the_attributes(ffmp):
+    """The footprint is cached per (map attributes, width) instead of rebuilt every call
+    (ffmp.py:87-94 rebuilds it): changing robot_rsize between calls still takes effect."""
+    m = np.zeros((100, 100), dtype=np.int32)
+    m[52, 50] = 255  # 0.10 m ahead of the robot cell
+    assert ffmp.is_collision(m)
+    ffmp.robot_rsize = 0.07
+    assert not ffmp.is_collision(m) and len(ffmp.robot_grids) == 5
+    ffmp.robot_rsize = 0.13
+    assert ffmp.is_collision(m) and len(ffmp.robot_grids) == 21
+    r, done = ffmp.rewarder(m, np.array([3.0, 0.1]), True)
+    assert done and r == -1.05

@@ -450,3 +450,26 @@ def test_env_lanes_identical(K, lanes_list):
         for k in first:
             if first[k] is not None:
                 assert np.array_equal(first[k], snaps[lanes][k], equal_nan=True), (lanes, k)
+
+
+def test_env_layout_falls_back_when_the_lds_does_not_fit():
+    """4 waves per block x 16 envs per wave (4 lanes, 4 discs per lane) at L = 1024 would
+    need 256 KiB of beam minima per block; the launch takes a layout that fits instead of failing,
+    and the results equal the default layout's and the oracle's."""
+    from flow_field_based_motion_planner_amd import _abi
+    cfg = FFMPConfig(grid=32, n_obst=16, n_beams=1024, moving=True, obst_rmax=0.5, obst_vmax=1.2, world_half=1.6,
+                     goal_max=1.2, max_steps=5, seed=45)
+    snaps = {}
+    for waves, lanes in ((1, 0), (4, 4)):
+        pw, pl = _abi.set_tuning(_abi.TUNE_ENV_WAVES, waves), _abi.set_tuning(_abi.TUNE_ENV_LANES, lanes)
+        try:
+            env, ref, problems, counts = _run(cfg, 37, 6, frame_window=3)
+        finally:
+            _abi.set_tuning(_abi.TUNE_ENV_WAVES, pw)
+            _abi.set_tuning(_abi.TUNE_ENV_LANES, pl)
+        assert not problems, (waves, lanes, problems[:5])
+        snaps[(waves, lanes)] = gpu_snapshot(env)
+    a, b = snaps[(1, 0)], snaps[(4, 4)]
+    for k in a:
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k], equal_nan=True), k

@@ -30,12 +30,27 @@ from flow_field_based_motion_planner_amd.learner import Brain  # noqa: E402
 from flow_field_based_motion_planner_amd.vec_env import FFMPVec  # noqa: E402
 
 
+def conv_flops(grid: int, cin: int) -> dict:
+    """Multiply-add FLOPs (x2) of the reference Network's convolutions per sample (train.py:234-237,
+    :244-255: conv1 cin -> 32 k 32, conv2 32 -> 64 k 32, conv3 64 -> 64 k 8, conv4 64 -> 64 k 8 three
+    times): forward, and backward = the data gradient of conv2-conv4 + the weight gradients of all."""
+    layers, h = [], grid
+    for c_in, c_out, k in [(cin, 32, 32), (32, 64, 32), (64, 64, 8), (64, 64, 8), (64, 64, 8), (64, 64, 8)]:
+        h = h - k + 1
+        layers.append(2.0 * h * h * c_out * c_in * k * k)
+    fwd = sum(layers)
+    return {"forward": fwd, "backward": 2 * fwd - layers[0]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=256)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--batch", type=int, default=256)         # train.py:62 uses 1024
-    ap.add_argument("--capacity", type=int, default=200_000)
+    ap.add_argument("--batch", type=int, default=256)         # train.py:63 uses 1024
+    ap.add_argument("--capacity", type=int, default=200_000)  # pfrl_train.py:65's; train.py:65 uses 20,000
+    ap.add_argument("--reference-hparams", action="store_true",
+                    help="the reference's own BATCH_SIZE = 1024 and CAPACITY = 20,000 (src/train.py:63-65), one "
+                         "update per step")
     ap.add_argument("--replay-every", type=int, default=1)
     ap.add_argument("--target-every", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
@@ -53,6 +68,8 @@ def main():
                     help="make_temporal_maps over --input-channels mono frames (train.py:474-486), from the frame ring")
     ap.add_argument("--warmup", type=int, default=3, help="untimed loop iterations (MIOpen compiles each conv shape once)")
     args = ap.parse_args()
+    if args.reference_hparams:
+        args.batch, args.capacity, args.replay_every = 1024, 20_000, 1
 
     dev = torch.device("cuda:0")
     # the reference map: 100x100 cells of 5 cm (ffmp.py:14-19), 200-step episodes (train.py:60)
@@ -95,7 +112,15 @@ def main():
     dt = t1 - t_warm
     env.check_errors()
     summ = tracker.summary()
+    timed_updates = sum(1 for s in range(args.warmup, args.warmup + args.steps) if s % args.replay_every == 0)
+    fl = conv_flops(cfg.grid, args.input_channels)
+    # acting: one forward of every env per step; a replay: Q(s) main, Q(s') main and target
+    # forwards of the batch, and the backward of Q(s) (data + weight gradients; conv1 has no data gradient)
+    conv_flop = args.steps * args.envs * fl["forward"] + timed_updates * args.batch * (3 * fl["forward"] +
+                                                                                      fl["backward"])
     out = {"env_steps_per_s": args.envs * args.steps / dt, "seconds": dt, "warmup_seconds": t_warm - t0,
+           "updates_per_s": timed_updates / dt, "conv_tflops_per_s": conv_flop / dt / 1e12,
+           "conv_gflop_per_sample": {k: round(v / 1e9, 3) for k, v in fl.items()},
            "envs": args.envs, "steps": args.steps, "amp": args.amp, "mfma": bool(brain.mfma and args.amp), "channels_last": args.channels_last,
            "input_channels": args.input_channels, "temporal_maps": args.temporal_maps,
            "learner_updates": updates, "batch": args.batch, "loss_samples": losses[:10],

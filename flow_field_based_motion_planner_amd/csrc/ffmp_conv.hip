@@ -747,6 +747,11 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
 // per kernel column) into the other buffer during the sweep and published by the phase's barrier.
 // Rows are dealt heaviest first (the middle output rows meet all KH kernel rows, the border rows
 // one), so the last workgroups to start are the short ones.
+// Measured and not kept (conv2's data gradient at B = 256, 1.59-1.62 ms with this code;
+// profiles/r05d_dgrad_ahead.txt, r05f_dgrad_variants.txt): A fragments read one valid position ahead
+// behind the guards (1.83 ms); B fragments and next-phase pieces over two register sets that swap
+// roles (1.63-1.64); one k-step per phase (2.26; with every valid position's A requested first 2.73);
+// 4 waves x 18 positions at one wave per SIMD (2.64); valid positions two at a time (490 spilled VGPRs).
 constexpr int kDgradNW = 8, kDgradPW = 9, kDgradKQ = 2;  // 72 output columns per row, 2 waves/SIMD
 
 template <int C, int N, int NW, int PW, int KQ>

@@ -67,6 +67,10 @@ def parse():
                    help="frame ring with frame_window > 2: seamless (VMM alias, never wraps) or wrap")
     p.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                    help="one-launch step (ffmp_step_fused) on/off, or auto: the instance's autotune decides")
+    p.add_argument("--graph", default="off", choices=["off", "on"],
+                   help="on: the timed steps run as replays of one HIP graph of graph_period() whole steps "
+                        "(FFMPVec.capture; no launch gaps or host work between kernels); the roofline's kernel "
+                        "is then the replayed step graph (env + raster kernels, their bytes)")
     p.add_argument("--save-tuning", default=None, help="write the instance's launch choices (JSON) here")
     p.add_argument("--tuning", default=None,
                    help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
@@ -370,14 +374,34 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     # ~10 % of a C2 step); the dominant kernel keeps its per-launch pairs (roofline.achieved)
     ev_loop = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     raster_ev = []
+    graph = None
+    if args.graph == "on" and main_leg and K >= env.graph_period():
+        # one graph of graph_period() whole steps, captured and replayed once (untimed, the warm-up's
+        # actions) before the timed region; the timed steps are K // period replays + K % period steps
+        graph = env.capture()
+        per = graph.steps
+        graph.replay(actions[:per])
+        torch.cuda.synchronize()
+        fulls = [env.frame_window == 2 or (env.ring != "seamless" and i == per - 1) for i in range(per)]
+        graph_bytes = sum(env._raster_bytes(n, f) + env._state_bytes(n) for f in fulls)
     ep0_t = env.episode.sum()  # read after the loop: no host round trip between the sync and the loop
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev_loop[0].record()
-    for k in range(K):
-        env.step(actions[W + k], timing=raster_ev)
+    if graph is None:
+        for k in range(K):
+            env.step(actions[W + k], timing=raster_ev)
+    else:
+        for r in range(K // per):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            graph.replay(actions[W + r * per:W + (r + 1) * per])
+            e1.record()
+            raster_ev.append((e0, e1, n, graph_bytes, False))
+        for k in range(K - K % per, K):
+            env.step(actions[W + k])
     ev_loop[1].record()
     torch.cuda.synchronize()
     if world > 1:
@@ -397,7 +421,11 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     n_full = sum(1 for r in raster_ev if r[4])
     G2 = cfg.grid * cfg.grid
     # resets spread evenly over the timed launches
-    r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / (K * env.pipeline_slices) * fb * G2
+    if graph is None:
+        r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / (K * env.pipeline_slices) * fb * G2
+    else:  # the replayed steps' newest-only rasters write an older frame for each env they reset
+        new_frac = sum(1 for f in fulls if not f) / per
+        r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) * per / K) * new_frac * fb * G2
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
@@ -417,9 +445,12 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
         "pool_released_bytes": getattr(env, "pool_released_bytes", 0),
         "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
+        "graph": None if graph is None else {"steps_per_replay": per, "replays": K // per, "eager_steps": K % per},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
-                     "kernel": "step_raster_kernel" if env.fused else "raster_kernel",
+                     "kernel": ("step graph (%s x %d steps)" % ("step_raster_kernel" if env.fused else
+                                                                 "env_kernel + raster_kernel", per)
+                                if graph is not None else "step_raster_kernel" if env.fused else "raster_kernel"),
                      "kernel_ms": sum(r_ms) / len(r_ms),
                      "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
                      "launches_per_step": env.pipeline_slices, "timed_launches": len(r_ms),
@@ -593,6 +624,7 @@ def main():
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
                        "frame_window": leg["frame_window"], "ring": leg["ring"], "fused": leg["fused"],
+                       "graph": leg["graph"],
                        "parallelism": f"env-shard x{world}",
                        "comm": (args.dist_backend if world > 1 else "none"), "world_size_backend": pg_world,
                        "launcher": ("bench.py" if os.environ.get("FFMP_BENCH_LAUNCHER") else

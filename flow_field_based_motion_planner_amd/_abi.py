@@ -130,6 +130,8 @@ _SIGS = {
     "ffmp_ring_destroy": (C.c_int, [_P]),
     "ffmp_ring_pool_bytes": (_I64, [_I32]),
     "ffmp_ring_pool_trim": (C.c_int, [_I32, _I64, C.POINTER(_I64)]),
+    "ffmp_ring_pair_forget": (C.c_int, [_I32, _P]),
+    "ffmp_ring_pair_refs": (C.c_int, [_I32]),
     "ffmp_dlpack": (_P, [_P, _I32, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64), _I32, _P]),
 }
 
@@ -227,6 +229,15 @@ def ring_pool_trim(device: int, keep_bytes: int = 0) -> int:
     out = C.c_int64(0)
     check(load().ffmp_ring_pool_trim(int(device), int(keep_bytes), C.byref(out)), "ffmp_ring_pool_trim")
     return int(out.value)
+
+
+def ring_pair_forget(device: int, partner: Optional[int] = None) -> int:
+    """Forget the ring-pairing references kept for the partner plane at address `partner` (None:
+    all of `device`'s), e.g. when the plane is freed (include/ffmp.h ffmp_ring_pair_forget)."""
+    rc = load().ffmp_ring_pair_forget(int(device), partner)
+    if rc < 0:
+        check(rc, "ffmp_ring_pair_forget")
+    return rc
 
 
 # ----------------------------------------------------------------- DLPack (device memory -> torch)

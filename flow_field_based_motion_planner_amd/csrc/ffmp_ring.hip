@@ -600,6 +600,25 @@ int64_t ffmp_ring_pool_bytes(int32_t device) {
   return b;
 }
 
+int ffmp_ring_pair_forget(int32_t device, const void* partner) {
+  if (device < 0) return fail(FFMP_E_ARG, "ffmp_ring_pair_forget: device must be >= 0");
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  const size_t before = g_pair_ref.size();
+  g_pair_ref.erase(std::remove_if(g_pair_ref.begin(), g_pair_ref.end(),
+                                  [device, partner](const PairRef& p) {
+                                    return p.device == device && (!partner || p.partner == partner);
+                                  }),
+                   g_pair_ref.end());
+  return (int)(before - g_pair_ref.size());
+}
+
+int ffmp_ring_pair_refs(int32_t device) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int n = 0;
+  for (const PairRef& p : g_pair_ref) n += p.device == device;
+  return n;
+}
+
 int ffmp_ring_pool_trim(int32_t device, int64_t keep_bytes, int64_t* released) {
   if (released) *released = 0;
   if (device < 0) return fail(FFMP_E_ARG, "ffmp_ring_pool_trim: device must be >= 0");
@@ -610,11 +629,8 @@ int ffmp_ring_pool_trim(int32_t device, int64_t keep_bytes, int64_t* released) {
   std::vector<ffmp_piece> victims;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    // the pairing references of this device are forgotten too: they are keyed by the partner
-    // plane's address, and a plane allocated later at the same address must not inherit them
-    g_pair_ref.erase(std::remove_if(g_pair_ref.begin(), g_pair_ref.end(),
-                                    [device](const PairRef& p) { return p.device == device; }),
-                     g_pair_ref.end());
+    // (the pairing references stay: live instances' rebuilds keep judging on their own scale; an
+    // owner forgets its partner plane's references when it frees the plane, ffmp_ring_pair_forget)
     int64_t kept = 0;
     for (size_t k = 0; k < g_pieces.size();) {
       ffmp_piece& p = g_pieces[k];

@@ -187,11 +187,15 @@ class FFMPVec:
             if self.placement is not None and self.ring_meta is not None:
                 self.placement = dict(self.placement, ring=self.ring_meta)
         self.pool_released_bytes = 0
+        if self.ring == "seamless":
+            # the pairing references of the planes this instance paired against and then dropped
+            # (relocation tries): those planes are freed, a later plane may take their address
+            self._forget_partners(keep=self.potential)
         if self.release_pool and self.ring == "seamless":
             # the pairing candidates this instance did not choose, the rings its relocation /
             # repair dropped: their memory goes back to the device (addresses stay reserved)
             torch.cuda.synchronize(self.device)
-            self.pool_released_bytes = _abi.ring_pool_trim(self.device.index, 0)
+            self.pool_released_bytes = _abi.ring_pool_trim(self.device.index, self.pool_keep_bytes)
             if self.ring_meta is not None:
                 self.ring_meta = dict(self.ring_meta, pool_released_bytes=self.pool_released_bytes)
                 if self.placement is not None and "ring" in self.placement:
@@ -201,8 +205,24 @@ class FFMPVec:
     # ------------------------------------------------------------------ setup
     # After construction (and on close) the frame-ring pieces parked in the process pool — pairing
     # candidates not chosen, rings dropped by the relocation / slot repair — are released
-    # (ffmp_ring_pool_trim): at C3 they were ~65 GB beside the instance's 77 GB (round 3).
+    # (ffmp_ring_pool_trim): at C3 they were ~65 GB beside the instance's 77 GB (round 3).  A
+    # process that builds envs in a loop may keep a floor of pieces for the next one (reused first).
     release_pool = True
+    pool_keep_bytes = 0
+    _pair_partners = ()  # potential-plane addresses this instance's rings were paired against
+
+    def _note_partner(self) -> None:
+        if self.potential is not None:
+            self._pair_partners = tuple(set(self._pair_partners) | {self.potential.data_ptr()})
+
+    def _forget_partners(self, keep: Optional[torch.Tensor] = None) -> None:
+        """Forget the ring-pairing references of the partner planes this instance no longer holds
+        (trimming the pool had erased every instance's)."""
+        k = None if keep is None else keep.data_ptr()
+        for ptr in self._pair_partners:
+            if ptr != k:
+                _abi.ring_pair_forget(self.device.index, ptr)
+        self._pair_partners = () if k is None else (k,)
 
     OBS_FORMATS = {"f32": (_abi.OBS_F32, torch.float32, torch.float32),
                    "u8f16": (_abi.OBS_U8F16, torch.uint8, torch.float16)}
@@ -324,6 +344,8 @@ class FFMPVec:
                                                partner=partner)
             self.frames = self._ring.tensor
             self.ring_meta = self._ring.info()
+            if partner is not None:
+                self._note_partner()
         except _abi.FFMPBackendError as e:
             # only a device without virtual memory management falls back to the wrapping ring;
             # any other failure (out of memory, a fault) is the caller's to see
@@ -1348,11 +1370,12 @@ class FFMPVec:
         self.bev = None
         had_ring = self.ring == "seamless"
         self._ring = None  # the seamless ring's pieces return to the process pool ...
+        self._forget_partners()  # the potential plane is freed: its pairing references go
         torch.cuda.empty_cache()
         if had_ring and self.release_pool:
             import gc
             gc.collect()  # ... once the last tensor view of the ring is gone
-            _abi.ring_pool_trim(self.device.index, 0)  # ... and their memory to the device
+            _abi.ring_pool_trim(self.device.index, self.pool_keep_bytes)  # ... and their memory to the device
 
     _closed = False
     bev = None  # the BEV image ring (bev_series); a class default: _alloc's HBM accounting runs first

@@ -474,14 +474,21 @@ int64_t ffmp_ring_pool_bytes(int32_t device);
  * write them are drained first), every mapping of such a piece — its home mapping and the slots
  * of the dead rings that held it — is unmapped and its handle released.  The address ranges
  * stay reserved until exit, so no later mapping is ever placed at an address that once held
- * another allocation (the stale-resolution hazard above).  Rings still alive are untouched.
- * The device's pairing references (the best probe seen per partner plane, keyed by the plane's
- * address) are forgotten as well, so a plane allocated later at a freed plane's address starts
- * its own.  *released (optional) = bytes given back.  Returns 0, FFMP_E_ARG or FFMP_E_HIP.
- * (FFMPVec calls it after construction and on close: an instance's unchosen pairing candidates
- * and the pieces of rings it dropped go back to the device.)  Replaces no reference interface:
- * the reference keeps its 2-frame stack as a host NumPy array (src/train.py:474-486). */
+ * another allocation (the stale-resolution hazard above).  Rings still alive are untouched, and
+ * so are the pairing references (see ffmp_ring_pair_forget).  *released (optional) = bytes given
+ * back.  Returns 0, FFMP_E_ARG or FFMP_E_HIP.  (FFMPVec calls it after construction and on close,
+ * keeping FFMPVec.pool_keep_bytes: an instance's unchosen pairing candidates and the pieces of
+ * rings it dropped go back to the device.)  Replaces no reference interface: the reference keeps
+ * its 2-frame stack as a host NumPy array (src/train.py:474-486). */
 int ffmp_ring_pool_trim(int32_t device, int64_t keep_bytes, int64_t* released);
+/* The pairing references — the best two-stream probe seen per (device, partner plane), the
+ * early-accept bar of ffmp_ring_create / ffmp_ring_rebuild — are keyed by the partner plane's
+ * address.  The owner of a partner plane forgets its references when it frees the plane (a plane
+ * allocated later at the same address must not inherit them): ffmp_ring_pair_forget(device,
+ * partner), partner NULL = every reference of the device.  Returns the number forgotten (>= 0) or
+ * FFMP_E_ARG.  ffmp_ring_pair_refs: how many the device holds. */
+int ffmp_ring_pair_forget(int32_t device, const void* partner);
+int ffmp_ring_pair_refs(int32_t device);
 /* A dlpack.h (v0.8) DLManagedTensor* of `bits` elements (8: uint8, 16/32/64: float) over `data` (element strides,
  * ndim <= 8), for consumers that take DLPack (torch.utils.dlpack.from_dlpack, CuPy, JAX).
  * Its deleter frees it and, when `owner` is a ring, drops the reference it took on it: a ring

@@ -67,10 +67,11 @@ def parse():
                    help="frame ring with frame_window > 2: seamless (VMM alias, never wraps) or wrap")
     p.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                    help="one-launch step (ffmp_step_fused) on/off, or auto: the instance's autotune decides")
-    p.add_argument("--graph", default="off", choices=["off", "on"],
-                   help="on: the timed steps run as replays of one HIP graph of graph_period() whole steps "
-                        "(FFMPVec.capture; no launch gaps or host work between kernels); the roofline's kernel "
-                        "is then the replayed step graph (env + raster kernels, their bytes)")
+    p.add_argument("--graph", default="on", choices=["off", "on"],
+                   help="on (default): the timed steps run as replays of one HIP graph of graph_period() whole "
+                        "steps (FFMPVec.capture: the same env + raster launches as step(), no launch gaps or host "
+                        "work between them); the roofline's kernel is then the replayed step graph (its env and "
+                        "raster kernels, their bytes).  off: one step() call per step")
     p.add_argument("--save-tuning", default=None, help="write the instance's launch choices (JSON) here")
     p.add_argument("--tuning", default=None,
                    help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
@@ -187,18 +188,21 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32"):
-    """(HBM bytes per raster launch, the profile file it came from) from the committed rocprofv3 PMC
-    summary, if one matches this launch; (None, None) otherwise."""
-    b = _load_traffic(workload, n_envs, window, ring, fused, obs_format)
+def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32",
+                 graph_steps: int = 0):
+    """(HBM bytes per timed launch, the profile file it came from) from the committed rocprofv3 PMC
+    summary, if one matches this launch — the raster (or one-launch step) kernel, or with
+    graph_steps > 0 one replay of that many whole steps; (None, None) otherwise."""
+    b = _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps)
     return b if b is not None else (None, None)
 
 
-def _load_traffic(workload, n_envs, window, ring, fused, obs_format):
+def _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps=0):
     label = f"{workload}{'' if obs_format == 'f32' else '_' + obs_format}"
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{'_fused' if fused else ''}.json")
+    gsfx = "_graph" if graph_steps else ""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{'_fused' if fused else ''}{gsfx}.json")
     if not os.path.exists(path):  # the one-launch and two-launch steps are profiled separately
-        path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}.json")
+        path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{gsfx}.json")
     if not os.path.exists(path):
         return None
     try:
@@ -206,9 +210,10 @@ def _load_traffic(workload, n_envs, window, ring, fused, obs_format):
             d = json.load(f)
         if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window \
                 or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused \
-                or d.get("obs_format", "f32") != obs_format:
+                or d.get("obs_format", "f32") != obs_format or int(d.get("graph_steps", 0)) != int(graph_steps):
             return None
-        return float(d["raster_hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        key = "step_graph_hbm_bytes_per_replay" if graph_steps else "raster_hbm_bytes_per_launch"
+        return float(d[key]), os.path.relpath(path, ROOT)
     except Exception:  # noqa: BLE001
         return None
 
@@ -374,16 +379,32 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     # ~10 % of a C2 step); the dominant kernel keeps its per-launch pairs (roofline.achieved)
     ev_loop = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     raster_ev = []
-    graph = None
-    if args.graph == "on" and main_leg and K >= env.graph_period():
+    graph, graph_error = None, None
+    if args.graph == "on" and K >= env.graph_period() and env.pipeline_slices == 1:
         # one graph of graph_period() whole steps, captured and replayed once (untimed, the warm-up's
         # actions) before the timed region; the timed steps are K // period replays + K % period steps
-        graph = env.capture()
+        try:
+            graph = env.capture()
+        except Exception as exc:  # noqa: BLE001 — a box whose runtime refuses the capture: step() instead
+            print(f"warning: HIP graph capture failed, timing step() calls instead: {exc}", file=sys.stderr)
+            graph_error = str(exc)[:300]
+    graph_rem = None
+    if graph is not None:
         per = graph.steps
-        graph.replay(actions[:per])
-        torch.cuda.synchronize()
+        rem = K % per
         fulls = [env.frame_window == 2 or (env.ring != "seamless" and i == per - 1) for i in range(per)]
         graph_bytes = sum(env._raster_bytes(n, f) + env._state_bytes(n) for f in fulls)
+        # the last K % period steps: a graph of their own, captured from the same position (each
+        # timed step is a replayed step); warmed once like the full one, then the ring is stepped back
+        # to the start (untimed)
+        graph.replay(actions[:per])
+        if rem:
+            graph_rem = env.capture(rem)
+            rem_bytes = sum(env._raster_bytes(n, f) + env._state_bytes(n) for f in fulls[:rem])
+            graph_rem.replay(actions[:rem])
+            for k in range(rem, per):
+                env.step(actions[k])
+        torch.cuda.synchronize()
     ep0_t = env.episode.sum()  # read after the loop: no host round trip between the sync and the loop
     if world > 1:
         dist.barrier()
@@ -400,8 +421,12 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
             graph.replay(actions[W + r * per:W + (r + 1) * per])
             e1.record()
             raster_ev.append((e0, e1, n, graph_bytes, False))
-        for k in range(K - K % per, K):
-            env.step(actions[W + k])
+        if graph_rem is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            graph_rem.replay(actions[W + K - rem:W + K])
+            e1.record()
+            raster_ev.append((e0, e1, n, rem_bytes, False))
     ev_loop[1].record()
     torch.cuda.synchronize()
     if world > 1:
@@ -425,7 +450,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) - n_full) / (K * env.pipeline_slices) * fb * G2
     else:  # the replayed steps' newest-only rasters write an older frame for each env they reset
         new_frac = sum(1 for f in fulls if not f) / per
-        r_bytes = sum(r[3] for r in raster_ev) + resets * (len(raster_ev) * per / K) * new_frac * fb * G2
+        r_bytes = sum(r[3] for r in raster_ev) + resets * new_frac * fb * G2
     b = bytes_per_env_step(cfg, potential=not args.no_potential, window=env.frame_window,
                            seamless=env.ring == "seamless", obs_format=args.obs_format)
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
@@ -445,14 +470,18 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
         "pool_released_bytes": getattr(env, "pool_released_bytes", 0),
         "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
-        "graph": None if graph is None else {"steps_per_replay": per, "replays": K // per, "eager_steps": K % per},
+        "graph": ({"steps_per_replay": per, "replays": K // per, "remainder_steps": rem} if graph is not None else
+                  {"error": graph_error} if graph_error else None),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "kernel": ("step graph (%s x %d steps)" % ("step_raster_kernel" if env.fused else
                                                                  "env_kernel + raster_kernel", per)
                                 if graph is not None else "step_raster_kernel" if env.fused else "raster_kernel"),
-                     "kernel_ms": sum(r_ms) / len(r_ms),
-                     "algorithmic_bytes_per_launch": r_bytes / len(raster_ev),
+                     # with graph replays: per replay of `per` steps (the full-period replays; a shorter
+                     # remainder replay counts in `achieved` only)
+                     "kernel_ms": (sum(r_ms[:K // per]) / (K // per)) if graph is not None else sum(r_ms) / len(r_ms),
+                     "algorithmic_bytes_per_launch": (r_bytes * per / K) if graph is not None else
+                                                     r_bytes / len(raster_ev),
                      "launches_per_step": env.pipeline_slices, "timed_launches": len(r_ms),
                      "full_launches": n_full, "timed_resets": resets},
         "raster_ms_per_step": sum(r_ms) / K,
@@ -572,7 +601,7 @@ def main():
     K, W = args.steps, args.warmup
     leg, env = run_leg(args, name, cfg, n, rank * n, K, W, dev, world, rank, strong, True)
     traffic, traffic_source = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused,
-                                           args.obs_format)
+                                           args.obs_format, (leg["graph"] or {}).get("steps_per_replay", 0))
     _release(env)
     env = None
 

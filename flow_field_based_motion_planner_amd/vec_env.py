@@ -1455,8 +1455,9 @@ class StepGraph:
     """`steps` consecutive FFMPVec steps captured as one HIP graph (FFMPVec.capture).
 
     The env kernel + raster (or the one-launch step) of each step are recorded with the frame-ring
-    slots that step writes; since `steps` is a multiple of graph_period(), the ring is back on its
-    starting slots after a replay and the same graph is valid for the next one.  replay(actions)
+    slots that step writes; when `steps` is a multiple of graph_period() the ring is back on its
+    starting slots after a replay and the same graph is valid for the next one (other counts replay
+    whenever the frame position is back where the capture started).  replay(actions)
     copies the (steps, N) action block into the graph's static block (one device copy), replays,
     then advances the env's host-side frame bookkeeping exactly as `steps` calls of step() would.
     Results are those of `steps` step() calls with the same actions, bit for bit
@@ -1472,8 +1473,11 @@ class StepGraph:
             raise ValueError("capture() needs pipeline=1 and no bev_series")
         per = env.graph_period()
         k = per if steps is None else int(steps)
-        if k <= 0 or k % per:
-            raise ValueError(f"steps must be a positive multiple of graph_period() = {per}")
+        if k <= 0:
+            raise ValueError("steps must be positive")
+        # a multiple of the period ends on the slots it started from, so it replays back to back;
+        # any other count is replayable once the frame position is back at the capture's
+        self.chainable = k % per == 0
         self.env, self.steps = env, k
         self.actions = torch.zeros((k, env.num_envs), dtype=torch.int64, device=env.device)
         snap = (env._wpos, list(env._hist), env._hist_from_reset)

@@ -42,7 +42,7 @@ def test_graph_replay_equals_steps(window, seamless, fused):
         b.step(acts[k])
     g = a.capture()
     with pytest.raises(ValueError):
-        a.capture(per + 1) if per > 1 else a.capture(0)
+        a.capture(0)
     for r in range(4):
         blk = acts[3 + r * per:3 + (r + 1) * per]
         g.replay(blk)
@@ -53,9 +53,29 @@ def test_graph_replay_equals_steps(window, seamless, fused):
         for k in sb:
             assert np.array_equal(sa[k], sb[k], equal_nan=True), (r, k)
     assert int(a.done.sum()) >= 0 and int(b.episode.sum()) > 0  # resets happened inside the replays
-    a.step(acts[0])  # the frame position moves: the graph refuses until a whole period has passed
     if per > 1:
+        # a partial graph (fewer steps than the period) replays from the capture's position once
+        part = a.capture(per - 1)
+        assert not part.chainable
+        blk = acts[:per - 1]
+        part.replay(blk)
+        for k in range(per - 1):
+            b.step(blk[k])
+        torch.cuda.synchronize()
+        sa, sb = _snap(a), _snap(b)
+        for k in sb:
+            assert np.array_equal(sa[k], sb[k], equal_nan=True), ("partial", k)
+        # the frame position moved: both graphs refuse until it is back where they were captured
         with pytest.raises(RuntimeError):
             g.replay()
+        a.step(acts[0])
+        b.step(acts[0])
+        g.replay(acts[1:per + 1])
+        for k in range(1, per + 1):
+            b.step(acts[k])
+        torch.cuda.synchronize()
+        sa, sb = _snap(a), _snap(b)
+        for k in sb:
+            assert np.array_equal(sa[k], sb[k], equal_nan=True), ("after partial", k)
     a.close()
     b.close()

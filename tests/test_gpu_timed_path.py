@@ -60,8 +60,11 @@ def test_timed_path_full_size_bit_exact(fmt):
     from flow_field_based_motion_planner_amd.vec_env import FFMPVec
     fused = FFMPVec.FUSED_FLAGS if fmt == "f32" else FFMPVec.COMPACT_FUSED_FLAGS
     shapes = FFMPVec.RASTER_SHAPES if fmt == "f32" else FFMPVec.COMPACT_SHAPES
-    used_fused = {f for kind, f in out["launches"] if kind == "fused"}
-    used_two = {tuple(s) for kind, s in out["launches"] if kind == "two"}
+    used_fused = {ln[1] for ln in out["launches"] if ln[0] == "fused"}
+    used_two = {tuple(ln[1]) for ln in out["launches"] if ln[0] == "two"}
+    # and the timed loop's own form: a whole ring cycle replayed from one HIP graph, both step kinds
+    graphs = [ln for ln in out["launches"] if ln[0].startswith("graph")]
+    assert {ln[0] for ln in graphs} == {"graph-two", "graph-fused"} and all(ln[2] == W for ln in graphs), graphs
     assert used_fused == set(fused), sorted(set(fused) - used_fused)
     assert used_two >= set(shapes), sorted(set(shapes) - used_two)
     if fmt == "f32":

@@ -18,7 +18,10 @@ kept in place).  One instance, built the way bench.py builds it from a tuning, t
     shape behind the round-3 driver bench).  max_steps = 6 truncates and auto-resets every env inside a newest-only
     launch (both frames of every env written that step); collisions / goals reset single envs on
     other steps;
-  * after the reset and after every step, ALL envs are compared in 4,096-env slices: state_m (both
+  * then (round 5) the step as bench.py's timed loop runs it: one HIP graph of a whole ring cycle
+    (FFMPVec.capture) of the tuned two-launch step and of the tuned one-launch step, each replayed
+    twice;
+  * after the reset and after every step / replay, ALL envs are compared in 4,096-env slices: state_m (both
     frames, read through the ring view), the potential plane, the raster record, t, episode and the
     flags bit-exact; the float outputs within tests/parity_util.py's tolerances, and their exact
     mismatch counts reported.
@@ -184,6 +187,33 @@ def main() -> int:
         problems += check(env, ref, fmt, f"step {k} ({stats['launches'][-1]})", stats)
         log(f"step {k} {stats['launches'][-1]}: slot {stats['slots_written'][-1]}, "
             f"{len(problems)} problems, {stats['resets']} resets so far")
+    # bench.py's timed loop replays one HIP graph of a whole ring cycle (FFMPVec.capture, --graph):
+    # the tuned two-launch step and the tuned one-launch step, each captured from where the eager
+    # plan left the ring and replayed twice, all envs checked after every replay
+    for fused in (False, True):
+        if problems:
+            break
+        env.fused = fused
+        if fused:
+            env.fused_flags = int(TUNING[fmt]["fused_flags"])
+        else:
+            env.raster_shape_newest = tuple(TUNING[fmt]["shape_newest"])
+        g = env.capture()
+        for r in range(2):
+            if problems:
+                break
+            acts = rng.integers(0, 28, (g.steps, n))
+            ep0 = int(env.episode.sum())
+            g.replay(torch.as_tensor(acts, device="cuda:0"))
+            for a in acts:
+                ref.step(a)
+            torch.cuda.synchronize()
+            how = ["graph-fused", int(env.fused_flags)] if fused else ["graph-two", list(env.raster_shape_newest)]
+            stats["launches"].append(how + [g.steps])
+            stats["resets"] += int(env.episode.sum()) - ep0
+            problems += check(env, ref, fmt, f"graph replay {r} ({how})", stats)
+            log(f"graph replay {r} {how} x {g.steps} steps: {len(problems)} problems, {stats['resets']} resets so far")
+        del g
     env.check_errors()
     out = {"ok": not problems, "obs_format": fmt, "n_envs": n, "frame_window": W, "ring": env.ring,
            "steps": len(plan), "problems": problems[:20], "ring_meta": env._ring.info(), **stats,

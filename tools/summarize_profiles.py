@@ -9,7 +9,8 @@
                                           raster: mean over the pass's timed launches (the frame
                                           window mixes full and newest-only launches), other
                                           kernels: median over dispatches
-  profiles/pmc_traffic_<cfg>[_fused].json what bench.py reads for roofline.traffic
+  profiles/pmc_traffic_<cfg>[_fused][_graph].json what bench.py reads for roofline.traffic (_graph:
+                                          per replay of the timed HIP graph, its env kernels + rasters)
 """
 import csv
 import glob
@@ -50,13 +51,25 @@ def counters(path, name):
     return per
 
 
+def graph_steps(bj) -> int:
+    """Steps per replay when bench.py timed HIP-graph replays (config.graph), else 0."""
+    return int(((bj or {}).get("config", {}).get("graph") or {}).get("steps_per_replay", 0) or 0)
+
+
 def timed_launches(log):
+    """Raster (or one-launch step) dispatches bench.py timed: one per step (per slice), or with
+    graph replays one per replayed step."""
     bj = bench_json(log) if os.path.exists(log) else None
-    return bj["steps"] * bj["roofline"].get("launches_per_step", 1) if bj else None
+    if not bj:
+        return None
+    g = graph_steps(bj)
+    if g:
+        return bj["config"]["graph"]["replays"] * g + bj["config"]["graph"].get("remainder_steps", 0)
+    return bj["steps"] * bj["roofline"].get("launches_per_step", 1)
 
 
-def per_launch(vals, key, k):
-    if key == "raster_kernel" and k:
+def per_launch(vals, key, k, graph=False):
+    if (key == "raster_kernel" or (graph and key == "env_kernel")) and k:
         tail = vals[-k:]
         return sum(tail) / len(tail)
     return statistics.median(vals)
@@ -77,12 +90,13 @@ def main():
     r = counters(find(f"pmcf_{cfg}/**/run_counter_collection.csv"), "FETCH_SIZE")
     kw = timed_launches(os.path.join(PROF, f"bench_pmcw_{cfg}.log"))
     kf = timed_launches(os.path.join(PROF, f"bench_pmcf_{cfg}.log"))
+    gs = graph_steps(bj)
     pm = {"workload": cfg, "units": "bytes per launch (raster: mean over the timed launches; others: median)",
           "correction": "WRITE_SIZE*1024 exact for 16-B/lane streaming stores; FETCH_SIZE*1024*2 (gfx950 halves wide "
                         "streaming reads, MI355X_MICROARCH.md HBM section)", "kernels": {}}
     for k in sorted(set(w) | set(r)):
-        wb = per_launch(w.get(k, [0.0]), k, kw) * 1024
-        fb = per_launch(r.get(k, [0.0]), k, kf) * 1024 * 2
+        wb = per_launch(w.get(k, [0.0]), k, kw, bool(gs)) * 1024
+        fb = per_launch(r.get(k, [0.0]), k, kf, bool(gs)) * 1024 * 2
         pm["kernels"][k] = {"write_bytes": wb, "fetch_bytes_corrected": fb, "hbm_bytes": wb + fb,
                             "dispatches": len(w.get(k, []))}
     if bj:
@@ -97,16 +111,49 @@ def main():
         pm["raster_algorithmic_bytes_per_launch"] = alg
         if "raster_kernel" in pm["kernels"]:
             hb = pm["kernels"]["raster_kernel"]["hbm_bytes"]
-            pm["raster_traffic_over_algorithmic"] = hb / alg
-            # bench.py looks the one-launch step up under its own label first
             sfx = "_fused" if pm["fused"] else ""
+            rec = {"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
+                   "obs_format": bj["config"].get("obs_format", "f32"), "raster_hbm_bytes_per_launch": hb,
+                   "source": f"{tag}_{cfg}_pmc.json"}
+            if gs:
+                # the timed unit is one replay of gs whole steps: their env kernels and rasters
+                eb = pm["kernels"].get("env_kernel", {}).get("hbm_bytes", 0.0)
+                pm["graph_steps"] = gs
+                pm["step_graph_hbm_bytes_per_replay"] = gs * (hb + eb)
+                pm["step_graph_traffic_over_algorithmic"] = gs * (hb + eb) / alg
+                rec.update(graph_steps=gs, step_graph_hbm_bytes_per_replay=gs * (hb + eb))
+                sfx += "_graph"
+            else:
+                pm["raster_traffic_over_algorithmic"] = hb / alg
+            # bench.py looks the one-launch step up under its own label first
             with open(os.path.join(OUT, f"pmc_traffic_{cfg}{sfx}.json"), "w") as f:
-                json.dump({"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
-                           "obs_format": bj["config"].get("obs_format", "f32"),
-                           "raster_hbm_bytes_per_launch": hb,
-                           "source": f"{tag}_{cfg}_pmc.json"}, f, indent=1)
+                json.dump(rec, f, indent=1)
     trace = find(f"trace_{cfg}/**/run_kernel_trace.csv")
-    if trace and bj:
+    if trace and bj and gs:
+        # each timed replay = gs consecutive steps of (env kernel, raster) or (one-launch step):
+        # its duration in the trace = first dispatch's start to last dispatch's end
+        rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r["Kernel_Name"] or
+                "env_kernel" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        per_step = 1 if pm["fused"] else 2
+        R = bj["config"]["graph"]["replays"]
+        rem = bj["config"]["graph"].get("remainder_steps", 0) * per_step  # a shorter last replay
+        timed = rows[len(rows) - rem - R * gs * per_step:len(rows) - rem]
+        reps = [timed[i * gs * per_step:(i + 1) * gs * per_step] for i in range(R)]
+        durs = [int(rp[-1]["End_Timestamp"]) - int(rp[0]["Start_Timestamp"]) for rp in reps]
+        busy = [sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in rp) for rp in reps]
+        pm["graph_timed_replays"] = R
+        pm["graph_replay_avg_ns_kernel_trace"] = sum(durs) / len(durs)
+        pm["graph_replay_kernel_busy_avg_ns"] = sum(busy) / len(busy)  # the kernels' own durations
+        pm["graph_replay_avg_ns_bench_events"] = bj["roofline"]["kernel_ms"] * 1e6
+        pm["trace_vs_events"] = pm["graph_replay_avg_ns_kernel_trace"] / pm["graph_replay_avg_ns_bench_events"]
+        ras = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in timed if "raster_kernel" in x["Kernel_Name"]]
+        env_ = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in timed if "env_kernel" in x["Kernel_Name"]]
+        pm["raster_avg_ns_kernel_trace"] = sum(ras) / max(len(ras), 1)
+        if env_:
+            pm["env_kernel_avg_ns_kernel_trace"] = sum(env_) / len(env_)
+        pm["raster_kernel_name"] = timed[-1]["Kernel_Name"]
+    elif trace and bj:
         # the last (steps x launches_per_step) raster dispatches are exactly the launches bench.py
         # timed; earlier ones are warm-up and the per-instance launch-shape autotune
         rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r["Kernel_Name"]]

@@ -456,7 +456,10 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     achieved = r_bytes / (sum(r_ms) * 1e-3) / 1e9
     # one all_gather of every rank's record after the timed region (the max-reduce of the timings
     # is its first column)
-    per_rank = _gather_floats(rank_record(el_local, construct_s, n, sum(r_ms) / len(r_ms), achieved / PEAK_HBM_GBS, env),
+    # the dominant kernel's mean launch: per step's raster (or one-launch step), or with graph
+    # replays per full-period replay (a shorter remainder replay counts in `achieved` only)
+    kernel_ms = (sum(r_ms[:K // per]) / (K // per)) if graph is not None else sum(r_ms) / len(r_ms)
+    per_rank = _gather_floats(rank_record(el_local, construct_s, n, kernel_ms, achieved / PEAK_HBM_GBS, env),
                               world, dev, args.dist_backend)
     el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
     n_total = int(sum(r[2] for r in per_rank))
@@ -479,7 +482,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
                                 if graph is not None else "step_raster_kernel" if env.fused else "raster_kernel"),
                      # with graph replays: per replay of `per` steps (the full-period replays; a shorter
                      # remainder replay counts in `achieved` only)
-                     "kernel_ms": (sum(r_ms[:K // per]) / (K // per)) if graph is not None else sum(r_ms) / len(r_ms),
+                     "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": (r_bytes * per / K) if graph is not None else
                                                      r_bytes / len(raster_ev),
                      "launches_per_step": env.pipeline_slices, "timed_launches": len(r_ms),

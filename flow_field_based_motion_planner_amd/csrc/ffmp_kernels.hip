@@ -912,6 +912,15 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
       for (int cb = wave % ncb; cb < ncb; cb += 4) {
         const int jb = cb * C, j = jb + cl;
         const float by0 = (float)jb * res - half, by1 = (float)(jb + C - 1) * res - half;
+        // the cull's column-band part per lane (disc): what is left of the reach^2 for the row
+        // distance, so a band's test is dx^2 <= tc — the same box test as box_dist2 <= rc2 up to
+        // float rounding (~1e-7 of rc^2), which the cull margin (0.1 m, i.e. ~0.1 of rc^2) covers
+        // many times over: culling stays conservative.  One VGPR per frame instead of the reach^2
+        // and the column term (the loop had spilled those and, reloading them, waited for every
+        // store of the previous band: vmcnt(0))
+        const float dyc = fmaxf(fmaxf(by0 - oc.y, oc.y - by1), 0.0f);
+        const float dyp = fmaxf(fmaxf(by0 - op.y, op.y - by1), 0.0f);
+        const float tc = rc2 - dyc * dyc, tp = rp2 - dyp * dyp;
         f2 ey2[NP], dyy2[NP];
 #pragma unroll
         for (int p2 = 0; p2 < NP; ++p2) {
@@ -924,8 +933,13 @@ FFMP_DEV __attribute__((always_inline)) void raster_env(const ffmp_cfg_t& cfg, i
           const int i = i0 + r;
           const int q = i * G + j;
           const float bx0 = (float)i0 * res - half, bx1 = (float)(i0 + R - 1) * res - half;
-          const uint64_t mc = __ballot(has && box_dist2(oc.x, oc.y, bx0, bx1, by0, by1) <= rc2);
-          const uint64_t mp = write_old ? __ballot(has && box_dist2(op.x, op.y, bx0, bx1, by0, by1) <= rp2) : 0ull;
+          const float dxc = fmaxf(fmaxf(bx0 - oc.x, oc.x - bx1), 0.0f);
+          const uint64_t mc = __ballot(has && dxc * dxc <= tc);
+          uint64_t mp = 0ull;
+          if (write_old) {
+            const float dxp = fmaxf(fmaxf(bx0 - op.x, op.x - bx1), 0.0f);
+            mp = __ballot(has && dxp * dxp <= tp);
+          }
           const uint64_t wb = __ballot(lane >= 8 || corner_inside(cfg, hq, (lane & 1) ? bx1 : bx0,
                                                                    (lane & 2) ? by1 : by0));
           const bool walls_c = (wb & 0xFull) != 0xFull;

@@ -15,9 +15,10 @@ runs on a batch of env tensors already in HBM:
 
 The linears are library GEMMs (hipBLASLt through torch).  With `mfma=True` and under bfloat16
 autocast (Brain(amp=True)), every convolution + ReLU runs on the hand-written MFMA kernels instead
-of MIOpen (conv_mfma.py, include/ffmp.h ffmp_conv2d_fwd_bf16 / ffmp_conv2d_wgrad_bf16: the
-forward, the data gradient and the weight gradient; conv1's 1-4 map channels with its kernel
-columns folded into channels, its input gradient — never needed by the Network — MIOpen's):
+of MIOpen (conv_mfma.py, include/ffmp.h ffmp_conv2d_fwd_bf16 / ffmp_conv2d_dgrad_bf16 /
+ffmp_conv2d_wgrad_bf16: the forward, the data gradient and the weight gradient; conv1's 1-16 map
+channels — the reference's 1 / 2 / 3 and the 12-channel BEV series, conv_mfma.fold_supported — with
+its kernel columns folded into 32 channels, its input gradient — never needed by the Network — MIOpen's):
 bf16 operands and fp32 accumulation like autocast's conv2d (the bias added in fp32, where
 autocast rounds it to bf16 first).  A layer whose input shape the kernels do not take
 (conv_mfma.supported / fold_supported with the shape: e.g. 64-channel rows over 16 KiB at

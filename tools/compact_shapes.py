@@ -1,6 +1,7 @@
 """Compact-format (uint8 frames, float16 potential) newest-only raster at C3 for a list of launch
 shapes, on ONE instance (no autotune): mean raster ms per launch over 2 x 8 steps of the real step
-loop (HIP events around each raster launch).  Usage: python tools/compact_shapes.py [cfg] [f32|u8f16]"""
+loop (HIP events around each raster launch).  Usage: python tools/compact_shapes.py [cfg] [f32|u8f16]
+[blocks:flags,...] [reps] (default: the SHAPES list below, 2 reps)"""
 import os
 import sys
 
@@ -23,12 +24,16 @@ SHAPES = [(65536, NT | T4 | NAR), (65536, NT | T2 | NAR),
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "C3"
     fmt = sys.argv[2] if len(sys.argv) > 2 else "u8f16"
+    shapes = SHAPES
+    if len(sys.argv) > 3 and sys.argv[3]:
+        shapes = [tuple(int(v) for v in t.split(":")) for t in sys.argv[3].split(",")]
+    reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     pr = PRESETS[name]
     n = pr["n_envs"] // max(1, pr["gpus"])
     env = FFMPVec(n, name, device="cuda:0", obs_format=fmt, autotune=False, fused=False)
     a = torch.full((n,), 10, dtype=torch.int64, device="cuda:0")
-    for rep in range(2):
-        for shape in SHAPES:
+    for rep in range(reps):
+        for shape in shapes:
             env.raster_shape = env.raster_shape_newest = shape
             env.reset()
             for _ in range(2):

@@ -28,6 +28,9 @@ def timeit(fn, reps=20):
 
 w = (torch.randn(64, 32, 32, 32, device=dev) / 181.0).to(torch.bfloat16)
 wp = pack_weight(w)
+if os.environ.get("FFMP_SWEEP_WFRAG"):  # probe builds reading B in fragment order: [tap][nb][s][h][r][8]
+    KH, KW, N, C = wp.shape
+    wp = wp.view(KH * KW, N // 32, 32, C // 16, 2, 8).permute(0, 1, 3, 4, 2, 5).contiguous().view(KH, KW, N, C)
 bias = torch.randn(64, device=dev)
 for B in [int(a) for a in (sys.argv[1:] or ["128", "170", "171", "256", "340", "342", "512", "1024"])]:
     xn = torch.relu(torch.randn(B, 69, 69, 32, device=dev)).to(torch.bfloat16)

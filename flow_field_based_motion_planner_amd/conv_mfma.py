@@ -163,6 +163,36 @@ def conv2d_wgrad_nhwc(g: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dx: in
     return part.sum(0) if chunks > 1 else part[0]
 
 
+def packed(weight: torch.Tensor, kind: str, fn) -> torch.Tensor:
+    """fn(weight) — a kernel-layout copy of a layer's weight — cached on the weight tensor until the
+    weight changes (its in-place version counter: optimizer steps and load_state_dict bump it).  One
+    training step runs the online network three times (acting, Q(s), Q(s')) and packs its weights
+    once; the target network's packs live until the next sync."""
+    stamp = (weight._version, weight.data_ptr())
+    cache = getattr(weight, "_ffmp_packs", None)
+    if cache is None:
+        cache = {}
+        try:
+            weight._ffmp_packs = cache
+        except (AttributeError, RuntimeError):  # a tensor that takes no attributes: no cache
+            return fn(weight)
+    hit = cache.get(kind)
+    if hit is not None and hit[0] == stamp:
+        return hit[1]
+    v = fn(weight)
+    cache[kind] = (stamp, v)
+    return v
+
+
+def relu_masked_nhwc(gy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """The ReLU's backward in one kernel: gy (NCHW-shaped, channels-last strides) where the NHWC
+    output y > 0, else 0, as a contiguous bf16 NHWC tensor."""
+    g = gy.permute(0, 2, 3, 1)
+    if g.dtype != torch.bfloat16:
+        g = g.to(torch.bfloat16)
+    return torch.ops.aten.threshold_backward(g, y, 0).contiguous()
+
+
 class MFMAConv2dReLU(torch.autograd.Function):
     """relu(conv2d(x, weight, bias)) in bf16 with fp32 accumulation; returns a bf16 NCHW-shaped
     tensor (channels-last strides).  The bias is added in fp32 (autocast's conv2d rounds it to
@@ -171,7 +201,7 @@ class MFMAConv2dReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
         xb = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # NHWC (free if x is channels-last)
-        wb = pack_weight(weight)
+        wb = packed(weight, "fwd", pack_weight)
         y = conv2d_nhwc(xb, wb, bias, relu=True, out_dtype=torch.bfloat16)
         ctx.save_for_backward(xb, weight, y)
         ctx.has_bias = bias is not None
@@ -181,16 +211,17 @@ class MFMAConv2dReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy: torch.Tensor):
         xb, weight, y = ctx.saved_tensors
-        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).contiguous()  # NHWC, masked by the ReLU
+        g = relu_masked_nhwc(gy, y)  # NHWC, masked by the ReLU
         need = ctx.needs_input_grad
         gx = gw = gb = None
         if need[0]:  # the full convolution of g with the flipped, transposed kernel, on the matrix cores
             N, Cin, KH, KW = weight.shape
             B, Hy, Wy, _ = g.shape
             if dgrad_bm_ok(B, Hy, Wy, N, KH, KW, Cin):  # 32 samples per MFMA block: no zero products
-                gx = conv2d_dgrad_nhwc(g, pack_weight_dgrad_bm(weight))
+                gx = conv2d_dgrad_nhwc(g, packed(weight, "dgrad_bm", pack_weight_dgrad_bm))
             else:
-                gx = conv2d_nhwc(g, pack_weight_dgrad(weight), None, out_dtype=torch.bfloat16, pad=KH - 1)
+                gx = conv2d_nhwc(g, packed(weight, "dgrad", pack_weight_dgrad), None, out_dtype=torch.bfloat16,
+                                 pad=KH - 1)
             gx = gx.permute(0, 3, 1, 2).to(ctx.x_dtype)
         if need[1]:  # on the matrix cores too: [KH][KW][N][C] -> torch's [N][C][KH][KW]
             gw = conv2d_wgrad_nhwc(g, xb, weight.shape[2], weight.shape[3]).permute(2, 3, 0, 1).to(weight.dtype)
@@ -262,7 +293,8 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
         F = 32 // x.shape[1]
-        y = conv2d_nhwc(fold_input(x, F), pack_weight_fold(weight, F), bias, relu=True, out_dtype=torch.bfloat16,
+        y = conv2d_nhwc(fold_input(x, F), packed(weight, f"fold{F}", lambda v: pack_weight_fold(v, F)), bias,
+                        relu=True, out_dtype=torch.bfloat16,
                         dx=F)
         ctx.save_for_backward(x, weight, y)
         ctx.has_bias = bias is not None
@@ -271,7 +303,7 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy: torch.Tensor):
         x, weight, y = ctx.saved_tensors
-        g = (gy.permute(0, 2, 3, 1).to(torch.bfloat16) * (y > 0)).contiguous()  # NHWC
+        g = relu_masked_nhwc(gy, y)  # NHWC
         need = ctx.needs_input_grad
         gx = gw = gb = None
         if need[0]:  # the map input has no gradient in the Network; for completeness, MIOpen's

@@ -1,0 +1,55 @@
+"""Host-side checks of conv_mfma's weight-pack cache and ReLU backward (CPU tensors; the kernels
+themselves are covered by tests/test_gpu_conv_mfma.py)."""
+import torch
+
+from flow_field_based_motion_planner_amd import conv_mfma
+
+
+def test_pack_cache_reuses_until_the_weight_changes():
+    conv = torch.nn.Conv2d(32, 64, kernel_size=4)
+    w = conv.weight
+    a = conv_mfma.packed(w, "fwd", conv_mfma.pack_weight)
+    assert conv_mfma.packed(w, "fwd", conv_mfma.pack_weight) is a
+    assert torch.equal(a, conv_mfma.pack_weight(w))
+    b = conv_mfma.packed(w, "dgrad_bm", conv_mfma.pack_weight_dgrad_bm)
+    assert b is not a and torch.equal(b, conv_mfma.pack_weight_dgrad_bm(w))
+    # an optimizer step (in-place update) invalidates every pack of the weight
+    opt = torch.optim.SGD(conv.parameters(), lr=0.1)
+    conv(torch.randn(2, 32, 8, 8)).sum().backward()
+    opt.step()
+    a2 = conv_mfma.packed(w, "fwd", conv_mfma.pack_weight)
+    assert a2 is not a and torch.equal(a2, conv_mfma.pack_weight(w))
+    assert not torch.equal(a2, a)
+    # so does load_state_dict (copy_ into the parameter)
+    conv.load_state_dict({k: torch.zeros_like(v) for k, v in conv.state_dict().items()})
+    a3 = conv_mfma.packed(w, "fwd", conv_mfma.pack_weight)
+    assert a3 is not a2 and int(a3.float().abs().sum()) == 0
+
+
+def test_pack_cache_without_attributes_falls_back():
+    class NoAttr(torch.Tensor):
+        def __setattr__(self, name, value):
+            raise AttributeError(name)
+    w = torch.randn(64, 32, 2, 2).as_subclass(NoAttr)
+    calls = []
+
+    def fn(v):
+        calls.append(1)
+        return conv_mfma.pack_weight(v.as_subclass(torch.Tensor))
+    conv_mfma.packed(w, "fwd", fn)
+    conv_mfma.packed(w, "fwd", fn)
+    assert len(calls) == 2
+
+
+def test_relu_backward_matches_mask_multiply():
+    torch.manual_seed(0)
+    y = torch.relu(torch.randn(3, 5, 6, 64)).to(torch.bfloat16)            # NHWC ReLU output
+    y[0, 0, 0, :4] = 0
+    gy = torch.randn(3, 64, 5, 6).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = conv_mfma.relu_masked_nhwc(gy, y)
+    ref = (gy.permute(0, 2, 3, 1) * (y > 0)).contiguous()
+    assert g.is_contiguous() and g.shape == (3, 5, 6, 64) and g.dtype == torch.bfloat16
+    assert torch.equal(g, ref)
+    # an fp32 incoming gradient is rounded to bf16 first, as before
+    g32 = conv_mfma.relu_masked_nhwc(gy.float(), y)
+    assert torch.equal(g32, ref)

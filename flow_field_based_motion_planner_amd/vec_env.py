@@ -25,6 +25,7 @@ step's return value (or `env.state_m`) rather than keeping the first one.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, Optional, Tuple, Union
 
 import numpy as np
@@ -1282,14 +1283,16 @@ class FFMPVec:
             return self.frame_window
         return self.frame_window - 1 if self.frame_window > 2 else 1
 
-    def capture(self, steps: Optional[int] = None) -> "StepGraph":
+    def capture(self, steps: Optional[int] = None, pipelined: Optional[bool] = None) -> "StepGraph":
         """Capture `steps` consecutive steps (default graph_period(); a multiple of it) into one HIP
         graph (torch.cuda.CUDAGraph: hipGraph on ROCm).  StepGraph.replay(actions) then runs them as
         ONE launch from the host — every kernel of every step, the same launches step() makes, with
         no host work or launch gaps between them; the actions are read from a static device block the
         replay fills first.  The host's frame bookkeeping is advanced by the replay, not by the
-        capture (nothing runs while capturing)."""
-        return StepGraph(self, steps)
+        capture (nothing runs while capturing).  `pipelined` (two-launch steps, an even count; off by
+        default, StepGraph.PIPELINE_DEFAULT): the env kernel of step i + 1 runs beside the raster of
+        step i (see StepGraph)."""
+        return StepGraph(self, steps, pipelined)
 
     # ------------------------------------------------ gym.vector.VectorEnv surface
     is_vector_env = True
@@ -1367,6 +1370,7 @@ class FFMPVec:
         self._state_c = self._obs_c = self._out_c = None
         self._slices = []
         self._arena_buf = None
+        self._record_alt = None
         self.bev = None
         had_ring = self.ring == "seamless"
         self._ring = None  # the seamless ring's pieces return to the process pool ...
@@ -1436,8 +1440,9 @@ class FFMPVec:
         ring = 0
         if self.ring == "seamless" and getattr(self, "_ring", None) is not None:
             ring = self.frame_window * self._ring.slot_stride
+        alt = getattr(self, "_record_alt", None)  # a pipelined step graph's second record buffer
         if self._arena_buf is not None:
-            return self._arena_buf.numel() + ring  # the BEV ring included (an arena buffer)
+            return self._arena_buf.numel() + ring + (0 if alt is None else alt.numel() * alt.element_size())
         return ring + sum(t.numel() * t.element_size() for t in vars(self).values()
                           if isinstance(t, torch.Tensor) and not (ring and t is self.frames))
 
@@ -1463,9 +1468,24 @@ class StepGraph:
     Results are those of `steps` step() calls with the same actions, bit for bit
     (tests/test_gpu_graph.py).  Not with pipeline slices or a BEV image ring (their launches need
     per-step host work), and the env must not be stepped or reset between capture and replay except
-    through whole replays or whole periods of step() calls (checked: the frame position)."""
+    through whole replays or whole periods of step() calls (checked: the frame position).
 
-    def __init__(self, env: FFMPVec, steps: Optional[int] = None):
+    Pipelined (two-launch steps, an even step count): the raster of step i reads only the record
+    its env kernel wrote, and the env kernel reads none of the raster's outputs, so with two record
+    buffers — step i's env kernel writes buffer (i + 1) % 2, the current record being buffer 0 —
+    the env kernel of step i + 1 runs on a second stream beside the raster of step i, waiting only
+    for the raster of step i - 1 (the last reader of its buffer).  The graph's intermediate steps'
+    small outputs (reward, done, state_g, ...) are overwritten one step early, which nobody sees: a
+    replay's observation is its last step's, written in the same order as step() writes it, and the
+    frames, potential and record are bit-identical (tests/test_gpu_graph.py)."""
+
+    # Off by default: the overlap happens (rocprofv3 trace, profiles/r05n_pipelined_graph.txt) but the
+    # raster beside an env kernel runs ~12 % longer and the graph leaves ~10 us between two rasters on
+    # different queues — C2 38.5-38.7 vs 38.9-39.2 M serial, C3 14.01-14.03 vs 13.88-14.03 M
+    # (profiles/r05m_pipelined_graph.txt).  FFMP_GRAPH_PIPELINE=1 makes it the default.
+    PIPELINE_DEFAULT = os.environ.get("FFMP_GRAPH_PIPELINE", "0") == "1"
+
+    def __init__(self, env: FFMPVec, steps: Optional[int] = None, pipelined: Optional[bool] = None):
         env._check_open()
         if env._needs_reset:
             raise RuntimeError("call reset() before capture()")
@@ -1480,23 +1500,64 @@ class StepGraph:
         self.chainable = k % per == 0
         self.env, self.steps = env, k
         self.actions = torch.zeros((k, env.num_envs), dtype=torch.int64, device=env.device)
+        can_pipe = not env.fused and k % 2 == 0
+        if pipelined is None:
+            pipelined = can_pipe and self.PIPELINE_DEFAULT
+        if pipelined and not can_pipe:
+            raise ValueError("a pipelined graph needs the two-launch step and an even step count")
+        self.pipelined = bool(pipelined)
         snap = (env._wpos, list(env._hist), env._hist_from_reset)
         self.wpos = env._wpos
         self.graph = torch.cuda.CUDAGraph()
         stream = torch.cuda.Stream(device=env.device)
         torch.cuda.synchronize(env.device)
-        with torch.cuda.device(env.device), torch.cuda.graph(self.graph, stream=stream):
-            for i in range(k):
-                if env.fused:
-                    env._step_fused(self.actions[i])
+        rec0 = env.record
+        if self.pipelined:
+            if getattr(env, "_record_alt", None) is None or env._record_alt.shape != rec0.shape:
+                env._record_alt = torch.empty_like(rec0)
+            bufs = (rec0, env._record_alt)
+            self._side = torch.cuda.Stream(device=env.device)
+        try:
+            with torch.cuda.device(env.device), torch.cuda.graph(self.graph, stream=stream):
+                if self.pipelined:
+                    self._capture_pipelined(k, bufs)
                 else:
-                    env.step_state(self.actions[i])
-                    env.raster_step()
-        # nothing ran: the host bookkeeping goes back to where the GPU state is
-        env._set_window(snap[0])
-        env._hist, env._hist_from_reset = snap[1], snap[2]
+                    for i in range(k):
+                        if env.fused:
+                            env._step_fused(self.actions[i])
+                        else:
+                            env.step_state(self.actions[i])
+                            env.raster_step()
+        finally:
+            env.record = rec0
+            env._state_c.record = rec0.data_ptr()
+            # nothing ran: the host bookkeeping goes back to where the GPU state is
+            env._set_window(snap[0])
+            env._hist, env._hist_from_reset = snap[1], snap[2]
         if env._wpos != self.wpos:
             raise RuntimeError("frame position changed during capture")
+
+    def _capture_pipelined(self, k: int, bufs) -> None:
+        env, side = self.env, self._side
+        cap = torch.cuda.current_stream(env.device)
+        fork = torch.cuda.Event()
+        fork.record(cap)
+        side.wait_event(fork)
+        ev_env = [torch.cuda.Event() for _ in range(k)]
+        ev_ras = [torch.cuda.Event() for _ in range(k)]
+        for i in range(k):
+            buf = bufs[(i + 1) % 2]  # k even: the last step writes buffer 0, the current record
+            env.record = buf
+            env._state_c.record = buf.data_ptr()
+            with torch.cuda.stream(side):
+                if i >= 2:
+                    side.wait_event(ev_ras[i - 2])  # the last raster that read this buffer
+                env.step_state(self.actions[i])
+                ev_env[i].record(side)
+            cap.wait_event(ev_env[i])
+            env.raster_step()
+            ev_ras[i].record(cap)
+        # the side stream's last work (env kernel k - 1) is joined by the last raster's wait
 
     def replay(self, actions: Optional[torch.Tensor] = None) -> None:
         """Run the captured steps; actions (steps, N) int64 (None: the block the last replay used)."""

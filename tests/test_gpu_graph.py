@@ -79,3 +79,55 @@ def test_graph_replay_equals_steps(window, seamless, fused):
             assert np.array_equal(sa[k], sb[k], equal_nan=True), ("after partial", k)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("window,seamless", [(8, True), (3, True), (4, False), (2, False)])
+def test_pipelined_graph_equals_steps(window, seamless):
+    """The pipelined graph (env kernel of step i + 1 beside the raster of step i, two record
+    buffers) against plain step() calls: same states, frames, potential and record after every
+    replay, bit for bit; odd step counts and the one-launch step refuse it."""
+    cfg = FFMPConfig(**CFG)
+    n = 96
+    kw = dict(device=DEV, frame_window=window, seamless=seamless if window > 2 else None, autotune=False)
+    a = FFMPVec(n, cfg, fused=False, **kw)
+    b = FFMPVec(n, cfg, fused=False, **kw)
+    per = a.graph_period()
+    k = per if per % 2 == 0 else 2 * per
+    rng = np.random.default_rng(9)
+    acts = torch.as_tensor(rng.integers(0, 28, (5 * k, n)), device=DEV)
+    a.reset()
+    b.reset()
+    for i in range(2):
+        a.step(acts[i])
+        b.step(acts[i])
+    g = a.capture(k, pipelined=True)
+    assert g.pipelined and g.chainable
+    if k % 2 == 0 and k > 1:
+        with pytest.raises(ValueError):
+            a.capture(k - 1, pipelined=True)
+    for r in range(4):
+        blk = acts[2 + r * k:2 + (r + 1) * k]
+        g.replay(blk)
+        for i in range(k):
+            b.step(blk[i])
+        torch.cuda.synchronize()
+        sa, sb = _snap(a), _snap(b)
+        for key in sb:
+            assert np.array_equal(sa[key], sb[key], equal_nan=True), (r, key)
+    assert int(b.episode.sum()) > 0  # resets happened inside the replays
+    # step() after replays keeps working on the same (current) record buffer
+    a.step(acts[0])
+    b.step(acts[0])
+    torch.cuda.synchronize()
+    sa, sb = _snap(a), _snap(b)
+    for key in sb:
+        assert np.array_equal(sa[key], sb[key], equal_nan=True), ("step after", key)
+    assert a.hbm_bytes() > b.hbm_bytes()  # the second record buffer is accounted
+    a.close()
+    b.close()
+    if window == 8:
+        f = FFMPVec(n, cfg, fused=True, **kw)
+        f.reset()
+        with pytest.raises(ValueError):
+            f.capture(k, pipelined=True)
+        f.close()

@@ -212,9 +212,24 @@ class FFMPVec:
     pool_keep_bytes = 0
     _pair_partners = ()  # potential-plane addresses this instance's rings were paired against
 
+    @staticmethod
+    def _forget_at_exit(device: int, box: list) -> None:
+        """weakref.finalize of an instance dropped without close(): its planes' pairing references
+        go with it (a later instance whose plane lands at the same address — torch's caching
+        allocator hands it out again — must not be judged against another plane's probe)."""
+        for ptr in box:
+            _abi.ring_pair_forget(device, ptr)
+        box.clear()
+
     def _note_partner(self) -> None:
         if self.potential is not None:
             self._pair_partners = tuple(set(self._pair_partners) | {self.potential.data_ptr()})
+            box = getattr(self, "_partner_box", None)
+            if box is None:
+                import weakref
+                box = self._partner_box = []
+                weakref.finalize(self, FFMPVec._forget_at_exit, self.device.index, box)
+            box[:] = list(self._pair_partners)
 
     def _forget_partners(self, keep: Optional[torch.Tensor] = None) -> None:
         """Forget the ring-pairing references of the partner planes this instance no longer holds
@@ -224,6 +239,9 @@ class FFMPVec:
             if ptr != k:
                 _abi.ring_pair_forget(self.device.index, ptr)
         self._pair_partners = () if k is None else (k,)
+        box = getattr(self, "_partner_box", None)
+        if box is not None:
+            box[:] = list(self._pair_partners)
 
     OBS_FORMATS = {"f32": (_abi.OBS_F32, torch.float32, torch.float32),
                    "u8f16": (_abi.OBS_U8F16, torch.uint8, torch.float16)}

@@ -72,6 +72,10 @@ def parse():
                         "steps (FFMPVec.capture: the same env + raster launches as step(), no launch gaps or host "
                         "work between them); the roofline's kernel is then the replayed step graph (its env and "
                         "raster kernels, their bytes).  off: one step() call per step")
+    p.add_argument("--graph-skew", default="auto", choices=["auto", "on", "off"],
+                   help="with --graph on: replay graphs whose steps are ONE launch each (the raster of step i + the "
+                        "env step of step i + 1, ffmp_step_skewed) — auto: time both graphs (3 alternating replays "
+                        "each, untimed) and keep the faster; on / off: force")
     p.add_argument("--save-tuning", default=None, help="write the instance's launch choices (JSON) here")
     p.add_argument("--tuning", default=None,
                    help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
@@ -379,15 +383,41 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     # ~10 % of a C2 step); the dominant kernel keeps its per-launch pairs (roofline.achieved)
     ev_loop = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     raster_ev = []
-    graph, graph_error = None, None
+    graph, graph_error, skew_trial = None, None, None
     if args.graph == "on" and K >= env.graph_period() and env.pipeline_slices == 1:
         # one graph of graph_period() whole steps, captured and replayed once (untimed, the warm-up's
         # actions) before the timed region; the timed steps are K // period replays + K % period steps
         try:
-            graph = env.capture()
+            from flow_field_based_motion_planner_amd.vec_env import StepGraph
+            per0 = env.graph_period()
+            can_skew = StepGraph.skew_supported(env, per0) and args.graph_skew != "off"
+            graph = env.capture(skewed=bool(can_skew and args.graph_skew == "on"))
+            if can_skew and args.graph_skew == "auto":
+                # the skewed graph (one launch per step) against the two-launch one: 3 alternating
+                # replays each after one warm replay, the faster (median) kept (C2: the env waves hide
+                # beside the raster; C3: 2,048 env blocks dispatched first delay the raster's stores)
+                gs = env.capture(skewed=True)
+                ms = {False: [], True: []}
+                for g in (graph, gs):
+                    g.replay(actions[:per0])
+                for _ in range(3):
+                    for key, g in ((False, graph), (True, gs)):
+                        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        a0.record()
+                        g.replay(actions[:per0])
+                        a1.record()
+                        torch.cuda.synchronize()
+                        ms[key].append(a0.elapsed_time(a1))
+                med = {key: sorted(v)[1] for key, v in ms.items()}
+                chosen = med[True] < 0.995 * med[False]
+                skew_trial = {"chosen": chosen, "serial_replay_ms": [round(v, 4) for v in ms[False]],
+                              "skewed_replay_ms": [round(v, 4) for v in ms[True]]}
+                if chosen:
+                    graph = gs
         except Exception as exc:  # noqa: BLE001 — a box whose runtime refuses the capture: step() instead
             print(f"warning: HIP graph capture failed, timing step() calls instead: {exc}", file=sys.stderr)
             graph_error = str(exc)[:300]
+            graph = None
     graph_rem = None
     if graph is not None:
         per = graph.steps
@@ -399,7 +429,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         # to the start (untimed)
         graph.replay(actions[:per])
         if rem:
-            graph_rem = env.capture(rem)
+            graph_rem = env.capture(rem, skewed=bool(graph.skewed and rem % 2 == 0))
             rem_bytes = sum(env._raster_bytes(n, f) + env._state_bytes(n) for f in fulls[:rem])
             graph_rem.replay(actions[:rem])
             for k in range(rem, per):
@@ -473,12 +503,14 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         "hbm_in_use_bytes": int(total - free), "hbm_total_bytes": int(total),
         "pool_released_bytes": getattr(env, "pool_released_bytes", 0),
         "frame_window": env.frame_window, "ring": env.ring, "fused": bool(env.fused),
-        "graph": ({"steps_per_replay": per, "replays": K // per, "remainder_steps": rem} if graph is not None else
+        "graph": ({"steps_per_replay": per, "replays": K // per, "remainder_steps": rem,
+                   "skewed": bool(graph.skewed), "skew_trial": skew_trial} if graph is not None else
                   {"error": graph_error} if graph_error else None),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "kernel": ("step graph (%s x %d steps)" % ("step_raster_kernel" if env.fused else
-                                                                 "env_kernel + raster_kernel", per)
+                                                                 "skew_kernel: raster i + env step i+1" if graph.skewed
+                                                                 else "env_kernel + raster_kernel", per)
                                 if graph is not None else "step_raster_kernel" if env.fused else "raster_kernel"),
                      # with graph replays: per replay of `per` steps (the full-period replays; a shorter
                      # remainder replay counts in `achieved` only)

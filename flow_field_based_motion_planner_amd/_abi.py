@@ -107,6 +107,8 @@ _SIGS = {
                             C.POINTER(OutT), _P]),
     "ffmp_step_fused": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, C.POINTER(StateT), C.POINTER(ObsT),
                                   C.POINTER(OutT), _I32, _P]),
+    "ffmp_step_skewed": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, C.POINTER(StateT), C.POINTER(ObsT),
+                                   C.POINTER(OutT), _P, _I32, _I32, _P]),
     "ffmp_reward_done": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P]),
     "ffmp_footprint_collision": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I64, _P, _P]),

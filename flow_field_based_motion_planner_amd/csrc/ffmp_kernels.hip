@@ -1169,6 +1169,81 @@ __global__ __launch_bounds__(256, (kFusedMinWaves<FLOW, FMT>)) void step_raster_
 #endif
 }
 
+// The skewed step (ffmp_step_skewed): ONE launch = the raster of step t (blocks env_blocks..) and the
+// env step of step t + 1 (blocks 0..env_blocks-1, four 64-lane env waves each, dispatched first),
+// which have no dependency on each other: the raster reads only step t's record (written by the
+// previous launch) and the env step writes step t + 1's state and its record into the OTHER record
+// buffer.  The env waves' float64 latency chains then run beside raster blocks' store streams
+// instead of as a launch of their own before the raster.  Float32 frames without flow planes: the
+// combined kernel keeps the stand-alone raster's occupancy (4 waves per SIMD: the env path's 116
+// VGPRs vs the raster's 108; 4 blocks per CU of LDS).  The two paths share one LDS block.
+template <int LPE>
+struct SkewEnvLds {
+  static constexpr int W = 4, DS = 64;
+  double ox[W][DS], oy[W][DS], orr_[W][DS], orrr[W][DS];
+  float4 ecur[W][DS], eprev[W][DS];
+  float2 foot[W][FFMP_MAX_FOOT + 1];
+  int pref[W][DS], lo[W][DS];
+};
+struct SkewRasterLds {
+  float4 cur[FFMP_MAX_OBST], prev[FFMP_MAX_OBST];
+  float2 vel[1];
+  float hdr[FFMP_REC_HDR];
+};
+
+template <bool NT, bool XCD, int LPE>
+__global__ __launch_bounds__(256) void skew_kernel(ffmp_cfg_t cfg, int64_t n, int64_t env_offset,
+                                                   const int64_t* __restrict__ action, ffmp_state_t st, ffmp_obs_t ob,
+                                                   ffmp_out_t out, int32_t env_chunks, int32_t chunk_s, int32_t bpe,
+                                                   int32_t cells_per_block, const float* __restrict__ record_r,
+                                                   int64_t sm_stride, int64_t sm_frame, int32_t newest_only,
+                                                   int32_t tile_log2r) {
+  constexpr int W = 4, EPW = 64 / LPE;
+  constexpr size_t kEnvB = sizeof(SkewEnvLds<LPE>), kRasB = sizeof(SkewRasterLds);
+  __shared__ __attribute__((aligned(16))) char smem[kEnvB > kRasB ? kEnvB : kRasB];
+  extern __shared__ uint32_t s_keys[];  // trace_discs' per-env beam minima (env blocks)
+  // Block layout: env_chunks chunks of [8 env blocks, 8 * chunk_s raster blocks], then the rest of the
+  // raster: the env blocks are spread over the first part of the launch (not all dispatched first —
+  // at C3 they would fill every block slot for two rounds with no store in flight), one per XCD per
+  // chunk, so each raster block keeps the XCD (blockIdx % 8) of its raster index.
+  const int64_t b = blockIdx.x, chunk = 8 * ((int64_t)chunk_s + 1);
+  int64_t env_block = -1, rb;
+  if (b < (int64_t)env_chunks * chunk) {
+    const int64_t c = b / chunk, off = b - c * chunk;
+    if (off < 8) env_block = c * 8 + off;
+    rb = c * 8 * chunk_s + (off - 8);
+  } else {
+    rb = (int64_t)env_chunks * 8 * chunk_s + (b - (int64_t)env_chunks * chunk);
+  }
+  if (env_block >= 0) {
+    SkewEnvLds<LPE>& L = *reinterpret_cast<SkewEnvLds<LPE>*>(smem);
+    const int wv = threadIdx.x >> 6;
+    const int grp = (threadIdx.x & 63) / LPE;
+    const int64_t e = (env_block * W + wv) * EPW + grp;
+    const int lane = threadIdx.x & (LPE - 1);
+    stage_footprint(cfg, L.foot[wv]);
+    if (e >= n) return;
+    const int g0 = grp * LPE;
+    env_group<kEnvMode_Step, LPE, FFMP_BEAM_CHUNK, true, 1>(
+        cfg, env_offset, action, 0, st, ob, out, e, lane, L.ox[wv] + g0, L.oy[wv] + g0, L.orr_[wv] + g0,
+        L.orrr[wv] + g0, L.ecur[wv] + g0, L.eprev[wv] + g0, L.foot[wv], nullptr, nullptr,
+        s_keys + ((size_t)wv * EPW + grp) * cfg.n_beams, L.pref[wv] + g0, L.lo[wv] + g0);
+    return;
+  }
+  SkewRasterLds& R = *reinterpret_cast<SkewRasterLds*>(smem);
+  // the raster's blocks as if they were a launch of their own
+  int64_t lb = rb;
+  if (XCD) {
+    const int64_t per = ((int64_t)gridDim.x - 8 * (int64_t)env_chunks) / 8;
+    if (lb < per * 8) lb = (lb % 8) * per + lb / 8;
+  }
+  const int64_t e = lb / bpe;
+  const int tile = (int)(lb - e * bpe);
+  if (e >= n) return;
+  raster_env<NT, false, FMT_F32>(cfg, e, tile, cells_per_block, record_r, ob.state_m, sm_stride, sm_frame, newest_only,
+                                 ob.potential, nullptr, tile_log2r, R.cur, R.prev, R.vel, R.hdr);
+}
+
 // ============================================================================
 // Legacy FFMP methods as batched kernels (one thread per env).
 // ============================================================================
@@ -1827,6 +1902,102 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
                        env_offset, action, *state, *obs, o, sm_stride, sm_frame, newest, tile_log2r);
   });
   return check_launch("ffmp_step_fused");
+}
+
+#ifndef FFMP_SKEW_ENV_SPAN
+// the share of the raster's blocks the env blocks are spread over: 0 = all dispatched first.  Spread
+// over the first quarter / half / 90 % they slowed the raster beside them (C3 13.3-13.5 M against
+// 13.9 front-loaded; C2 no better; profiles/r05s_skew_span.txt)
+#define FFMP_SKEW_ENV_SPAN 0.0
+#endif
+static constexpr double kSkewEnvSpan = FFMP_SKEW_ENV_SPAN;
+
+int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
+                     ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
+                     int32_t cells_per_block, int32_t flags, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0 || env_offset < 0) return fail(FFMP_E_ARG, "negative n or env_offset");
+  if (!state_next || !obs || !action_next || !out || !record_raster)
+    return fail(FFMP_E_ARG, "state/obs/action/out/record_raster is NULL");
+  if (!state_next->pose || !state_next->goal || !state_next->d0 || !state_next->t || !state_next->episode ||
+      !state_next->record || !state_next->err)
+    return fail(FFMP_E_ARG, "a state pointer is NULL");
+  if (state_next->record == record_raster)
+    return fail(FFMP_E_ARG, "ffmp_step_skewed: the env step must write the other record buffer");
+  if (cfg->n_obst > 0 && (!state_next->obst || !state_next->obst_r)) return fail(FFMP_E_ARG, "obstacle state NULL");
+  if (!obs->state_m || !obs->state_g || !obs->state_v || !obs->state_t || !obs->grad)
+    return fail(FFMP_E_ARG, "an obs pointer is NULL");
+  if (cfg->n_beams > 0 && !obs->lidar) return fail(FFMP_E_ARG, "obs.lidar NULL with n_beams > 0");
+  if (!out->reward || !out->done || !out->is_goal || !out->collide || !out->truncated)
+    return fail(FFMP_E_ARG, "an out pointer is NULL");
+  if ((flags & FFMP_RASTER_NT) && (flags & FFMP_RASTER_PLAIN)) return fail(FFMP_E_ARG, "NT and PLAIN both set");
+  if (cells_per_block != 0 && (cells_per_block < 1024 || cells_per_block % 1024 != 0))
+    return fail(FFMP_E_ARG, "cells_per_block must be 0 or a multiple of 1024, got %d", cells_per_block);
+  if (int rc2 = check_format(obs, cfg->flow != 0)) return rc2;
+  // the instances there are: float32 frames, no flow planes, one disc per lane on 8..64 lanes
+  if (obs->format != FFMP_OBS_F32 || cfg->flow) return fail(FFMP_E_ARG, "ffmp_step_skewed: float32 frames without flow planes only");
+  const int lpe = cfg->n_obst <= 8 ? 8 : cfg->n_obst <= 16 ? 16 : cfg->n_obst <= 32 ? 32 : 64;
+  if (n == 0) return FFMP_OK;
+  const int G2 = cfg->grid * cfg->grid;
+  const int cpb_max = cells_per_block ? cells_per_block : 4096;
+  const int cpb = G2 < cpb_max ? ((G2 + 1023) / 1024) * 1024 : cpb_max;
+  const int bpe = (G2 + cpb - 1) / cpb;
+  const int64_t env_per_block = 4 * (64 / lpe);
+  const int64_t env_chunks = ((n + env_per_block - 1) / env_per_block + 7) / 8;  // 8 env blocks each
+  const int64_t ras_blocks = n * bpe;
+  // the env blocks spread over the first kSkewEnvSpan of the raster's blocks
+  const int64_t chunk_s = std::max<int64_t>(0, (int64_t)(kSkewEnvSpan * (double)ras_blocks) / (8 * env_chunks));
+  if (ras_blocks + 8 * env_chunks > 0x7fffffffLL / 256) return fail(FFMP_E_ARG, "ffmp_step_skewed: n too large for one launch");
+  if (env_chunks * 8 * chunk_s > ras_blocks) return fail(FFMP_E_ARG, "ffmp_step_skewed: block layout");
+  const int64_t sm_stride = obs->state_m_stride ? obs->state_m_stride : 2 * (int64_t)G2;
+  const int64_t sm_frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : (int64_t)G2;
+  const int64_t sm_frame_abs = sm_frame < 0 ? -sm_frame : sm_frame;
+  if (sm_stride < (int64_t)G2 || sm_frame_abs < (int64_t)G2 ||
+      (sm_stride < 2 * (int64_t)G2 && sm_frame_abs < n * (int64_t)G2))
+    return fail(FFMP_E_ARG, "state_m strides overlap: env %lld, frame %lld elements (G*G = %d)", (long long)sm_stride,
+                (long long)sm_frame, G2);
+  const bool nt = (flags & FFMP_RASTER_NT) ? true : (flags & FFMP_RASTER_PLAIN) ? false : (G2 <= 16384);
+  const bool xcd = (flags & FFMP_RASTER_XCD) != 0;
+  const int32_t newest = (flags & FFMP_RASTER_NEWEST) ? 1 : 0;
+  int32_t tile_log2r = tile_rows_log2(flags);
+  if (tile_log2r) {
+    const int C = 256 >> tile_log2r, R = 1 << tile_log2r;
+    const bool whole_bands = cpb >= G2 || (cpb % (cfg->grid * R)) == 0;
+    if ((cfg->grid % C) != 0 || !whole_bands) tile_log2r = 0;
+  }
+  const size_t keys = (size_t)4 * (64 / lpe) * (size_t)cfg->n_beams * sizeof(uint32_t);
+  const dim3 grid((unsigned)(ras_blocks + 8 * env_chunks)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  ffmp_out_t o = *out;
+  auto go = [&](auto NT_, auto XCD_, auto L_) {
+    constexpr bool kNT = decltype(NT_)::value, kXCD = decltype(XCD_)::value;
+    constexpr int kL = decltype(L_)::value;
+    static const size_t static_lds = [] {
+      hipFuncAttributes a{};
+      return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&skew_kernel<kNT, kXCD, kL>)) == hipSuccess
+                 ? (size_t)a.sharedSizeBytes
+                 : (size_t)0;
+    }();
+    if (static_lds + keys > device_lds_limit()) return false;
+    hipLaunchKernelGGL((skew_kernel<kNT, kXCD, kL>), grid, block, keys, s, *cfg, n, env_offset, action_next, *state_next,
+                       *obs, o, (int32_t)env_chunks, (int32_t)chunk_s, bpe, cpb, record_raster, sm_stride, sm_frame,
+                       newest, tile_log2r);
+    return true;
+  };
+  using T = std::true_type;
+  using N = std::false_type;
+  auto with_l = [&](auto NT_, auto XCD_) {
+    switch (lpe) {
+      case 8: return go(NT_, XCD_, std::integral_constant<int, 8>{});
+      case 16: return go(NT_, XCD_, std::integral_constant<int, 16>{});
+      case 32: return go(NT_, XCD_, std::integral_constant<int, 32>{});
+      default: return go(NT_, XCD_, std::integral_constant<int, 64>{});
+    }
+  };
+  const bool ok = nt ? (xcd ? with_l(T{}, T{}) : with_l(T{}, N{})) : (xcd ? with_l(N{}, T{}) : with_l(N{}, N{}));
+  if (!ok) return fail(FFMP_E_ARG, "ffmp_step_skewed: the env waves' LDS does not fit (L = %d)", cfg->n_beams);
+  return check_launch("ffmp_step_skewed");
 }
 
 int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n, const double* scan, int32_t scan_len,

@@ -1301,7 +1301,8 @@ class FFMPVec:
             return self.frame_window
         return self.frame_window - 1 if self.frame_window > 2 else 1
 
-    def capture(self, steps: Optional[int] = None, pipelined: Optional[bool] = None) -> "StepGraph":
+    def capture(self, steps: Optional[int] = None, pipelined: Optional[bool] = None,
+                skewed: Optional[bool] = None) -> "StepGraph":
         """Capture `steps` consecutive steps (default graph_period(); a multiple of it) into one HIP
         graph (torch.cuda.CUDAGraph: hipGraph on ROCm).  StepGraph.replay(actions) then runs them as
         ONE launch from the host — every kernel of every step, the same launches step() makes, with
@@ -1309,8 +1310,10 @@ class FFMPVec:
         replay fills first.  The host's frame bookkeeping is advanced by the replay, not by the
         capture (nothing runs while capturing).  `pipelined` (two-launch steps, an even count; off by
         default, StepGraph.PIPELINE_DEFAULT): the env kernel of step i + 1 runs beside the raster of
-        step i (see StepGraph)."""
-        return StepGraph(self, steps, pipelined)
+        step i (see StepGraph).  `skewed` (float32 frames, no flow planes, the two-launch step, an even
+        count; by default where the env step's blocks fit the CUs once, StepGraph._skew_pays): the
+        raster of step i and the env step of step i + 1 in ONE launch (ffmp_step_skewed)."""
+        return StepGraph(self, steps, pipelined, skewed)
 
     # ------------------------------------------------ gym.vector.VectorEnv surface
     is_vector_env = True
@@ -1502,8 +1505,30 @@ class StepGraph:
     # different queues — C2 38.5-38.7 vs 38.9-39.2 M serial, C3 14.01-14.03 vs 13.88-14.03 M
     # (profiles/r05m_pipelined_graph.txt).  FFMP_GRAPH_PIPELINE=1 makes it the default.
     PIPELINE_DEFAULT = os.environ.get("FFMP_GRAPH_PIPELINE", "0") == "1"
+    SKEW_DEFAULT = os.environ.get("FFMP_GRAPH_SKEW", "1") != "0"  # A/B knob
 
-    def __init__(self, env: FFMPVec, steps: Optional[int] = None, pipelined: Optional[bool] = None):
+    @staticmethod
+    def skew_supported(env: FFMPVec, k: int) -> bool:
+        """Does ffmp_step_skewed take this instance's steps (include/ffmp.h: float32 frames, no flow
+        planes; its env waves' LDS: 22.5 KiB of disc arrays + 4 x envs-per-wave x L beam words)?"""
+        if env.fused or k % 2 or env.obs_format != "f32" or env.flow is not None:
+            return False
+        K = env.cfg.n_obst
+        lpe = 8 if K <= 8 else 16 if K <= 16 else 32 if K <= 32 else 64
+        return 22560 + 4 * (64 // lpe) * env.cfg.n_beams * 4 <= 64 * 1024
+
+    @staticmethod
+    def _skew_pays(env: FFMPVec) -> bool:
+        """The default: skew while the env step's blocks (4 waves each) fit the CUs once — they are
+        dispatched first, and more of them delay the raster's stores (C2's 128 blocks: 39.6 -> 41.2 M
+        env-steps/s; C3's 2,048: 14.0 -> 13.9 M; profiles/r05r_skewed_graph.txt).  bench.py times both."""
+        K = env.cfg.n_obst
+        lpe = 8 if K <= 8 else 16 if K <= 16 else 32 if K <= 32 else 64
+        blocks = -(-env.num_envs // (4 * (64 // lpe)))
+        return blocks <= torch.cuda.get_device_properties(env.device).multi_processor_count
+
+    def __init__(self, env: FFMPVec, steps: Optional[int] = None, pipelined: Optional[bool] = None,
+                 skewed: Optional[bool] = None):
         env._check_open()
         if env._needs_reset:
             raise RuntimeError("call reset() before capture()")
@@ -1524,21 +1549,31 @@ class StepGraph:
         if pipelined and not can_pipe:
             raise ValueError("a pipelined graph needs the two-launch step and an even step count")
         self.pipelined = bool(pipelined)
+        can_skew = not self.pipelined and self.skew_supported(env, k)
+        if skewed is None:
+            skewed = can_skew and self.SKEW_DEFAULT and self._skew_pays(env)
+        if skewed and not can_skew:
+            raise ValueError("a skewed graph needs the two-launch step, an even step count, float32 frames "
+                             "without flow planes, and no pipelining")
+        self.skewed = bool(skewed)
         snap = (env._wpos, list(env._hist), env._hist_from_reset)
         self.wpos = env._wpos
         self.graph = torch.cuda.CUDAGraph()
         stream = torch.cuda.Stream(device=env.device)
         torch.cuda.synchronize(env.device)
         rec0 = env.record
-        if self.pipelined:
+        if self.pipelined or self.skewed:
             if getattr(env, "_record_alt", None) is None or env._record_alt.shape != rec0.shape:
                 env._record_alt = torch.empty_like(rec0)
             bufs = (rec0, env._record_alt)
+        if self.pipelined:
             self._side = torch.cuda.Stream(device=env.device)
         try:
             with torch.cuda.device(env.device), torch.cuda.graph(self.graph, stream=stream):
                 if self.pipelined:
                     self._capture_pipelined(k, bufs)
+                elif self.skewed:
+                    self._capture_skewed(k, bufs)
                 else:
                     for i in range(k):
                         if env.fused:
@@ -1576,6 +1611,28 @@ class StepGraph:
             env.raster_step()
             ev_ras[i].record(cap)
         # the side stream's last work (env kernel k - 1) is joined by the last raster's wait
+
+    def _capture_skewed(self, k: int, bufs) -> None:
+        """env(0); then for i < k - 1 ONE launch of raster(i) + env(i + 1); then raster(k - 1).  env(i)
+        writes record buffer (i + 1) % 2, raster(i) reads it (k even: the last is buffer 0)."""
+        env = self.env
+        env.record = bufs[1]
+        env._state_c.record = bufs[1].data_ptr()
+        env.step_state(self.actions[0])
+        for i in range(k - 1):
+            full = env._next_window()
+            cpb, flags = env.raster_shape if full else env.raster_shape_newest
+            flags |= 0 if full else _abi.RASTER_NEWEST
+            rec_r, rec_w = bufs[(i + 1) % 2], bufs[(i + 2) % 2]
+            env.record = rec_w
+            env._state_c.record = rec_w.data_ptr()
+            _abi.check(env.lib.ffmp_step_skewed(C.byref(env._cfg_c), env.num_envs, env.env_offset,
+                                                self.actions[i + 1].data_ptr(), C.byref(env._state_c),
+                                                C.byref(env._obs_c), C.byref(env._out_c), rec_r.data_ptr(), cpb,
+                                                flags, env._stream()), "ffmp_step_skewed")
+        env.record = bufs[0]
+        env._state_c.record = bufs[0].data_ptr()
+        env.raster_step()
 
     def replay(self, actions: Optional[torch.Tensor] = None) -> None:
         """Run the captured steps; actions (steps, N) int64 (None: the block the last replay used)."""

@@ -254,6 +254,20 @@ int ffmp_raster_ex(const ffmp_cfg_t* cfg, int64_t n, const float* record,
 int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action,
                     ffmp_state_t* state, ffmp_obs_t* obs, ffmp_out_t* out, int32_t flags, void* stream);
 
+/* The raster of step t and the env step of step t + 1 in ONE launch (round 5): the raster reads
+ * record_raster (step t's record, written by the previous launch) and writes obs->state_m /
+ * potential as ffmp_raster_ex does (cells_per_block, flags: the same meaning); the env step reads
+ * action_next and advances state_next, whose record pointer must be the OTHER record buffer, and
+ * writes the small obs (state_g/v/t, grad, lidar) and out of step t + 1.  Nothing either half reads
+ * is written by the other, so the env waves' latency chains run beside raster blocks' stores.
+ * Within a sequence of steps whose intermediate small outputs nobody reads (a replayed step graph:
+ * ffmp_step_state of step 0 into buffer B, then this for t = 0 .. k-2 alternating the buffers, then
+ * ffmp_raster_ex of step k-1) every frame, plane, state and record equals k ffmp_step calls.
+ * Float32 frames without flow planes only (FFMP_E_ARG otherwise: run the two launches instead). */
+int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
+                     ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
+                     int32_t cells_per_block, int32_t flags, void* stream);
+
 /* ffmp_step_state + ffmp_raster. */
 int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
               const int64_t* action, ffmp_state_t* state, ffmp_obs_t* obs,

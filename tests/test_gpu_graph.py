@@ -131,3 +131,55 @@ def test_pipelined_graph_equals_steps(window, seamless):
         with pytest.raises(ValueError):
             f.capture(k, pipelined=True)
         f.close()
+
+
+@pytest.mark.parametrize("window,seamless,n_obst", [(8, True, 8), (8, True, 12), (3, True, 8), (4, False, 8),
+                                                    (2, False, 8), (8, True, 0)])
+def test_skewed_graph_equals_steps(window, seamless, n_obst):
+    """The skewed graph (ONE launch per step: raster of step i + env step of step i + 1,
+    ffmp_step_skewed, two record buffers) against plain step() calls: states, frames, potential,
+    record and the last step's small outputs bit for bit after every replay, for each ring layout,
+    8 and 16 lanes per env and no discs; the compact layout and odd counts refuse it."""
+    cfg = FFMPConfig(**dict(CFG, n_obst=n_obst))
+    n = 96
+    kw = dict(device=DEV, frame_window=window, seamless=seamless if window > 2 else None, autotune=False)
+    a = FFMPVec(n, cfg, fused=False, **kw)
+    b = FFMPVec(n, cfg, fused=False, **kw)
+    per = a.graph_period()
+    k = per if per % 2 == 0 else 2 * per
+    rng = np.random.default_rng(13)
+    acts = torch.as_tensor(rng.integers(0, 28, (3 + 5 * k, n)), device=DEV)
+    a.reset()
+    b.reset()
+    for i in range(3):
+        a.step(acts[i])
+        b.step(acts[i])
+    g = a.capture(k, skewed=True)
+    assert g.skewed and not g.pipelined and g.chainable
+    with pytest.raises(ValueError):
+        a.capture(k, skewed=True, pipelined=True)
+    for r in range(4):
+        blk = acts[3 + r * k:3 + (r + 1) * k]
+        g.replay(blk)
+        for i in range(k):
+            b.step(blk[i])
+        torch.cuda.synchronize()
+        sa, sb = _snap(a), _snap(b)
+        for key in sb:
+            assert np.array_equal(sa[key], sb[key], equal_nan=True), (r, key)
+    assert int(b.episode.sum()) > 0  # resets happened inside the replays
+    a.step(acts[0])
+    b.step(acts[0])
+    torch.cuda.synchronize()
+    sa, sb = _snap(a), _snap(b)
+    for key in sb:
+        assert np.array_equal(sa[key], sb[key], equal_nan=True), ("step after", key)
+    a.close()
+    b.close()
+    if window == 8 and n_obst == 8:
+        c = FFMPVec(n, cfg, fused=False, obs_format="u8f16", **kw)
+        c.reset()
+        assert not c.capture(k).skewed  # the default falls back to the two launches
+        with pytest.raises(ValueError):
+            c.capture(k, skewed=True)
+        c.close()

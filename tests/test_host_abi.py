@@ -78,6 +78,21 @@ def test_argument_validation_no_gpu(lib):
     out2 = _abi.OutT(p, p, p, p, p)
     assert lib.ffmp_step_state(C.byref(cfg), 0, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), None) == 0
     assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == 0
+    # the skewed step (raster of step t + env step of step t + 1): the env step must write the other
+    # record buffer; float32 frames without flow planes only; n == 0 launches nothing
+    other = C.cast((C.c_double * 8)(), C.c_void_p).value
+    assert lib.ffmp_step_skewed(C.byref(cfg), 0, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), other, 0, 0,
+                                None) == 0
+    assert lib.ffmp_step_skewed(C.byref(cfg), 4, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), p, 0, 0,
+                                None) == -1
+    assert b"other record buffer" in lib.ffmp_last_error()
+    assert lib.ffmp_step_skewed(C.byref(cfg), 4, 0, None, C.byref(st2), C.byref(ob2), C.byref(out2), other, 0, 0,
+                                None) == -1
+    ob2.format = _abi.OBS_U8F16
+    assert lib.ffmp_step_skewed(C.byref(cfg), 4, 0, p, C.byref(st2), C.byref(ob2), C.byref(out2), other, 0, 0,
+                                None) == -1
+    assert b"float32 frames" in lib.ffmp_last_error()
+    ob2.format = _abi.OBS_F32
     # observation formats (FFMP_OBS_*): unknown ones are refused; the compact one takes binary16 flow planes
     ob2.format = 7
     assert lib.ffmp_raster(C.byref(cfg), 0, p, None, C.byref(ob2), None) == -1

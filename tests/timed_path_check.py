@@ -19,7 +19,8 @@ kept in place).  One instance, built the way bench.py builds it from a tuning, t
     launch (both frames of every env written that step); collisions / goals reset single envs on
     other steps;
   * then (round 5) the step as bench.py's timed loop runs it: one HIP graph of a whole ring cycle
-    (FFMPVec.capture) of the tuned two-launch step and of the tuned one-launch step, each replayed
+    (FFMPVec.capture) of the tuned two-launch step, of the tuned one-launch step and (float32) of the
+    skewed step (raster i + env step i + 1 per launch), each replayed
     twice;
   * after the reset and after every step / replay, ALL envs are compared in 4,096-env slices: state_m (both
     frames, read through the ring view), the potential plane, the raster record, t, episode and the
@@ -190,7 +191,13 @@ def main() -> int:
     # bench.py's timed loop replays one HIP graph of a whole ring cycle (FFMPVec.capture, --graph):
     # the tuned two-launch step and the tuned one-launch step, each captured from where the eager
     # plan left the ring and replayed twice, all envs checked after every replay
-    for fused in (False, True):
+    # (and the skewed graph, ffmp_step_skewed — one launch per step — which bench.py keeps where it
+    # is faster: float32 frames only)
+    from flow_field_based_motion_planner_amd.vec_env import StepGraph
+    modes = [(False, False), (True, False)]
+    if StepGraph.skew_supported(env, env.graph_period()):
+        modes.append((False, True))
+    for fused, skewed in modes:
         if problems:
             break
         env.fused = fused
@@ -198,7 +205,7 @@ def main() -> int:
             env.fused_flags = int(TUNING[fmt]["fused_flags"])
         else:
             env.raster_shape_newest = tuple(TUNING[fmt]["shape_newest"])
-        g = env.capture()
+        g = env.capture(skewed=skewed)
         for r in range(2):
             if problems:
                 break
@@ -208,7 +215,8 @@ def main() -> int:
             for a in acts:
                 ref.step(a)
             torch.cuda.synchronize()
-            how = ["graph-fused", int(env.fused_flags)] if fused else ["graph-two", list(env.raster_shape_newest)]
+            how = (["graph-fused", int(env.fused_flags)] if fused else
+                   ["graph-skewed" if skewed else "graph-two", list(env.raster_shape_newest)])
             stats["launches"].append(how + [g.steps])
             stats["resets"] += int(env.episode.sum()) - ep0
             problems += check(env, ref, fmt, f"graph replay {r} ({how})", stats)

@@ -193,15 +193,15 @@ def _cpu_model() -> str:
 
 
 def load_traffic(workload: str, n_envs: int, window: int, ring: str, fused: bool, obs_format: str = "f32",
-                 graph_steps: int = 0):
+                 graph_steps: int = 0, graph_skewed: bool = False):
     """(HBM bytes per timed launch, the profile file it came from) from the committed rocprofv3 PMC
     summary, if one matches this launch — the raster (or one-launch step) kernel, or with
     graph_steps > 0 one replay of that many whole steps; (None, None) otherwise."""
-    b = _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps)
+    b = _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps, graph_skewed)
     return b if b is not None else (None, None)
 
 
-def _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps=0):
+def _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps=0, graph_skewed=False):
     label = f"{workload}{'' if obs_format == 'f32' else '_' + obs_format}"
     gsfx = "_graph" if graph_steps else ""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{label}{'_fused' if fused else ''}{gsfx}.json")
@@ -214,7 +214,8 @@ def _load_traffic(workload, n_envs, window, ring, fused, obs_format, graph_steps
             d = json.load(f)
         if int(d.get("n_envs", -1)) != n_envs or int(d.get("frame_window", 2)) != window \
                 or d.get("ring", "wrap" if window > 2 else "contiguous") != ring or bool(d.get("fused", False)) != fused \
-                or d.get("obs_format", "f32") != obs_format or int(d.get("graph_steps", 0)) != int(graph_steps):
+                or d.get("obs_format", "f32") != obs_format or int(d.get("graph_steps", 0)) != int(graph_steps) \
+                or bool(d.get("skewed", False)) != bool(graph_skewed and graph_steps):
             return None
         key = "step_graph_hbm_bytes_per_replay" if graph_steps else "raster_hbm_bytes_per_launch"
         return float(d[key]), os.path.relpath(path, ROOT)
@@ -636,7 +637,8 @@ def main():
     K, W = args.steps, args.warmup
     leg, env = run_leg(args, name, cfg, n, rank * n, K, W, dev, world, rank, strong, True)
     traffic, traffic_source = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused,
-                                           args.obs_format, (leg["graph"] or {}).get("steps_per_replay", 0))
+                                           args.obs_format, (leg["graph"] or {}).get("steps_per_replay", 0),
+                                           bool((leg["graph"] or {}).get("skewed", False)))
     _release(env)
     env = None
 

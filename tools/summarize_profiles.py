@@ -45,8 +45,10 @@ def counters(path, name):
                       key=lambda r: int(r["Dispatch_Id"]))
     for row in rows:
         k = row["Kernel_Name"]
-        # "raster_kernel" = the timed kernel: raster_kernel or step_raster_kernel (fused step)
-        key = "raster_kernel" if "raster_kernel" in k else ("env_kernel" if "env_kernel" in k else k)
+        # "raster_kernel" = the timed kernel: raster_kernel or step_raster_kernel (fused step);
+        # "skew_kernel": the skewed step's launch (raster of step i + env step of step i + 1)
+        key = ("skew_kernel" if "skew_kernel" in k else "raster_kernel" if "raster_kernel" in k else
+               "env_kernel" if "env_kernel" in k else k)
         per.setdefault(key, []).append(float(row["Counter_Value"]))
     return per
 
@@ -66,6 +68,29 @@ def timed_launches(log):
     if g:
         return bj["config"]["graph"]["replays"] * g + bj["config"]["graph"].get("remainder_steps", 0)
     return bj["steps"] * bj["roofline"].get("launches_per_step", 1)
+
+
+def step_kernels(path, name):
+    """(kernel key, value) of the step's own dispatches (env / raster / skew kernels) in dispatch order."""
+    with open(path) as f:
+        rows = sorted((r for r in csv.DictReader(f) if r.get("Counter_Name") == name and
+                       any(t in r["Kernel_Name"] for t in ("env_kernel", "raster_kernel", "skew_kernel"))),
+                      key=lambda r: int(r["Dispatch_Id"]))
+    return [("skew_kernel" if "skew_kernel" in r["Kernel_Name"] else "raster_kernel" if "raster_kernel" in
+             r["Kernel_Name"] else "env_kernel", float(r["Counter_Value"])) for r in rows]
+
+
+def replay_dispatches(bj, gs):
+    """(dispatches per full replay, dispatches of the remainder replay) of bench.py's timed graphs: per
+    step an env kernel + a raster (two-launch), one step kernel (fused), or env(0) + (gs - 1) skewed
+    launches + raster(gs - 1) (skewed)."""
+    g = bj["config"]["graph"]
+    rem = g.get("remainder_steps", 0)
+    if bj["config"].get("fused"):
+        return gs, rem
+    if g.get("skewed"):
+        return gs + 1, (rem + 1 if rem and rem % 2 == 0 else 2 * rem)
+    return 2 * gs, 2 * rem
 
 
 def per_launch(vals, key, k, graph=False):
@@ -115,7 +140,23 @@ def main():
             rec = {"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
                    "obs_format": bj["config"].get("obs_format", "f32"), "raster_hbm_bytes_per_launch": hb,
                    "source": f"{tag}_{cfg}_pmc.json"}
-            if gs:
+            if gs and (bj["config"]["graph"].get("skewed") or "skew_kernel" in pm["kernels"]):
+                # a skewed graph: the HBM bytes of the timed replays' own dispatches, per replay
+                per_rep, rem_d = replay_dispatches(bj, gs)
+                R = bj["config"]["graph"]["replays"]
+                tot = []
+                for name, path, scale in (("WRITE_SIZE", find(f"pmcw_{cfg}/**/run_counter_collection.csv"), 1024),
+                                          ("FETCH_SIZE", find(f"pmcf_{cfg}/**/run_counter_collection.csv"), 2048)):
+                    rows = step_kernels(path, name)
+                    timed = rows[len(rows) - rem_d - R * per_rep:len(rows) - rem_d]
+                    tot.append(sum(v for _, v in timed) * scale / R)
+                pm["graph_steps"] = gs
+                pm["skewed"] = True
+                pm["step_graph_hbm_bytes_per_replay"] = sum(tot)
+                pm["step_graph_traffic_over_algorithmic"] = sum(tot) / alg
+                rec.update(graph_steps=gs, step_graph_hbm_bytes_per_replay=sum(tot), skewed=True)
+                sfx += "_graph"
+            elif gs:
                 # the timed unit is one replay of gs whole steps: their env kernels and rasters
                 eb = pm["kernels"].get("env_kernel", {}).get("hbm_bytes", 0.0)
                 pm["graph_steps"] = gs
@@ -133,13 +174,14 @@ def main():
         # each timed replay = gs consecutive steps of (env kernel, raster) or (one-launch step):
         # its duration in the trace = first dispatch's start to last dispatch's end
         rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r["Kernel_Name"] or
-                "env_kernel" in r["Kernel_Name"]]
+                "env_kernel" in r["Kernel_Name"] or "skew_kernel" in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        per_step = 1 if pm["fused"] else 2
+        per_rep, rem = replay_dispatches(bj, gs)  # a shorter last replay: rem dispatches
         R = bj["config"]["graph"]["replays"]
-        rem = bj["config"]["graph"].get("remainder_steps", 0) * per_step  # a shorter last replay
-        timed = rows[len(rows) - rem - R * gs * per_step:len(rows) - rem]
-        reps = [timed[i * gs * per_step:(i + 1) * gs * per_step] for i in range(R)]
+        timed = rows[len(rows) - rem - R * per_rep:len(rows) - rem]
+        reps = [timed[i * per_rep:(i + 1) * per_rep] for i in range(R)]
+        gaps = [int(b_["Start_Timestamp"]) - int(a_["End_Timestamp"]) for rp in reps for a_, b_ in zip(rp, rp[1:])]
+        pm["graph_inter_kernel_gap_avg_ns"] = sum(gaps) / max(len(gaps), 1)
         durs = [int(rp[-1]["End_Timestamp"]) - int(rp[0]["Start_Timestamp"]) for rp in reps]
         busy = [sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in rp) for rp in reps]
         pm["graph_timed_replays"] = R
@@ -149,9 +191,12 @@ def main():
         pm["trace_vs_events"] = pm["graph_replay_avg_ns_kernel_trace"] / pm["graph_replay_avg_ns_bench_events"]
         ras = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in timed if "raster_kernel" in x["Kernel_Name"]]
         env_ = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in timed if "env_kernel" in x["Kernel_Name"]]
+        skw = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in timed if "skew_kernel" in x["Kernel_Name"]]
         pm["raster_avg_ns_kernel_trace"] = sum(ras) / max(len(ras), 1)
         if env_:
             pm["env_kernel_avg_ns_kernel_trace"] = sum(env_) / len(env_)
+        if skw:
+            pm["skew_kernel_avg_ns_kernel_trace"] = sum(skw) / len(skw)
         pm["raster_kernel_name"] = timed[-1]["Kernel_Name"]
     elif trace and bj:
         # the last (steps x launches_per_step) raster dispatches are exactly the launches bench.py

@@ -25,7 +25,7 @@ BENCH="$R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --w
 echo "== trace"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/trace_$LBL -o run -- python3 $BENCH > $R/gpurun_out/prof/bench_trace_$LBL.log 2>&1 || exit 1
 echo "== pmc write"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcw_$LBL.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcw_$LBL.log 2>&1 || exit 1
 echo "== pmc fetch"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcf_$LBL.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcf_$LBL.log 2>&1 || exit 1
 cd $R && python3 tools/summarize_profiles.py $TAG $LBL

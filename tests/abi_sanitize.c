@@ -144,6 +144,12 @@ int main(void) {
   EXPECT(ffmp_step_state(&cfg, 0, 0, act, &st2, &ob2, &out2, NULL) == FFMP_OK);
   EXPECT(ffmp_raster(&cfg, 0, (const float*)p, NULL, &ob2, NULL) == FFMP_OK);
   EXPECT(ffmp_step_fused(&cfg, 0, 0, act, &st2, &ob2, &out2, 0, NULL) == FFMP_OK);
+  {
+    /* the skewed step: the env step must write the other record buffer */
+    float other[4];
+    EXPECT(ffmp_step_skewed(&cfg, 0, 0, act, &st2, &ob2, &out2, other, 0, 0, NULL) == FFMP_OK);
+    EXPECT(ffmp_step_skewed(&cfg, 4, 0, act, &st2, &ob2, &out2, (const float*)p, 0, 0, NULL) == FFMP_E_ARG);
+  }
   ob2.format = 7;  /* unknown observation format */
   EXPECT(ffmp_raster(&cfg, 0, (const float*)p, NULL, &ob2, NULL) == FFMP_E_ARG);
   ob2.format = FFMP_OBS_U8F16;

@@ -288,6 +288,10 @@ void pool_put(const std::vector<ffmp_piece>& v) {
 // a two-stream probe at or above this is a well-paired piece (MI355X: 6.7-7.0 TB/s paired
 // well, 4.5-5.6 badly; tools/pair_alias_probe.hip)
 constexpr double kPairFastGBs = 6200.0;
+#ifndef FFMP_PAIR_ACCEPT
+#define FFMP_PAIR_ACCEPT 0.93  // a piece is taken when its probe is within this factor of the best seen
+#endif
+constexpr double kPairAccept = FFMP_PAIR_ACCEPT;
 
 // Pieces beyond the ones a ring needs (pairing candidates) only while the device keeps
 // max(8 GiB, 5 %) free beside them.
@@ -444,7 +448,7 @@ int choose_pieces(ffmp_ring* r, const RingGeom& g, const std::vector<char>& need
       // never below kPairFastGBs: slot 0's positions come first, and judged only against the
       // handful of probes seen so far they took badly paired pieces (round 2: slot 0 ~10 % slower
       // than every other slot on three boxes, and again after a rebuild)
-      if ((r->pieces_tested >= 3 || ref > kPairFastGBs) && pick_gbs >= std::max(0.93 * ref, kPairFastGBs)) break;
+      if ((r->pieces_tested >= 3 || ref > kPairFastGBs) && pick_gbs >= std::max(kPairAccept * ref, kPairFastGBs)) break;
       if (here >= 12) break;  // bounded search: keep the best seen
     }
     if (pick < 0) {

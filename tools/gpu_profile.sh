@@ -21,11 +21,19 @@ timeout -k 10 300 python3 -c "import sys; sys.path.insert(0,'$R'); import __graf
 echo "== tuning run"
 timeout -k 10 300 python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 8 --warmup 2 --cpu-seconds 0 --save-tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_tuning_$LBL.log 2>&1 || exit 1
 cat $R/gpurun_out/prof/tuning_$LBL.json; echo
-BENCH="$R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 10 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json"
+# the graph form the tuning run's skew trial kept (skewed or two-launch), forced in the profiled runs so that
+# every pass times the same kernels
+SKEW=$(python3 -c "
+import json
+ls = [l for l in open('$R/gpurun_out/prof/bench_tuning_$LBL.log') if l.startswith('{')]
+d = json.loads(ls[-1])
+print('on' if (d['config'].get('graph') or {}).get('skewed') else 'off')" 2>/dev/null || echo off)
+echo "graph skew: $SKEW"
+BENCH="$R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --graph-skew $SKEW --steps 48 --warmup 10 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json"
 echo "== trace"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/trace_$LBL -o run -- python3 $BENCH > $R/gpurun_out/prof/bench_trace_$LBL.log 2>&1 || exit 1
 echo "== pmc write"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcw_$LBL.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcw_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --graph-skew $SKEW --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcw_$LBL.log 2>&1 || exit 1
 echo "== pmc fetch"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcf_$LBL.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'raster_kernel|env_kernel|skew_kernel' --output-format csv -d $R/gpurun_out/prof/pmcf_$LBL -o run -- python3 $R/bench.py --config $CFG --obs-format $FMT --fused $FUSED --graph-skew $SKEW --steps 48 --warmup 2 --cpu-seconds 0 --tuning $R/gpurun_out/prof/tuning_$LBL.json > $R/gpurun_out/prof/bench_pmcf_$LBL.log 2>&1 || exit 1
 cd $R && python3 tools/summarize_profiles.py $TAG $LBL

@@ -140,7 +140,7 @@ def main():
             rec = {"n_envs": n, "frame_window": pm["frame_window"], "ring": pm["ring"], "fused": pm["fused"],
                    "obs_format": bj["config"].get("obs_format", "f32"), "raster_hbm_bytes_per_launch": hb,
                    "source": f"{tag}_{cfg}_pmc.json"}
-            if gs and (bj["config"]["graph"].get("skewed") or "skew_kernel" in pm["kernels"]):
+            if gs and bj["config"]["graph"].get("skewed"):  # (a skew trial alone leaves skew_kernel rows too)
                 # a skewed graph: the HBM bytes of the timed replays' own dispatches, per replay
                 per_rep, rem_d = replay_dispatches(bj, gs)
                 R = bj["config"]["graph"]["replays"]

@@ -19,6 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 ABI_VERSION = 7
 OBS_F32, OBS_U8F16 = 0, 1  # include/ffmp.h FFMP_OBS_*
 MAX_SERIES = 16  # FFMP_MAX_SERIES (ffmp_temporal_maps)
+PACKED_ARG_BEAMS = 360  # FFMP_PACKED_ARG_BEAMS (ffmp_reward_done_packed flag 8)
 
 
 class FFMPBackendError(RuntimeError):

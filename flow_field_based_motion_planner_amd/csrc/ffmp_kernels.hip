@@ -1278,6 +1278,34 @@ __global__ void reward_done_kernel(ffmp_cfg_t cfg, int64_t n, const double* __re
   collide[e] = col;
 }
 
+// One env's reward / done with its inputs in the kernel's arguments (ffmp_reward_done_packed flag 8):
+// no host -> device copy; the outputs go straight into the caller's pinned block through its device
+// view.  The same operations as reward_done_kernel for n = 1 without a local map.
+struct PackedArgs {
+  double scan[FFMP_PACKED_ARG_BEAMS];
+  double dist, d0, robot_r, goal_thr;
+  int32_t scan_len;
+  uint8_t is_first, collide_in, goal_in, flags;
+};
+__global__ void reward_done_args_kernel(PackedArgs a, uint8_t* __restrict__ out) {
+  // the beams over the wave's 64 lanes: "some beam hits" does not depend on the order it is tested in
+  bool hit = false;
+  for (int l = (int)threadIdx.x; l < a.scan_len; l += 64) {
+    const double r = a.scan[l];
+    hit = hit || (r != 0.0 && r < a.robot_r);
+  }
+  const bool any_hit = __ballot(hit) != 0ull;
+  if (threadIdx.x != 0) return;
+  const bool col = ((a.flags & 1) ? (a.collide_in != 0) : false) || any_hit;
+  const bool goal = (a.flags & 2) ? (a.goal_in != 0) : (a.dist < a.goal_thr);
+  const double d0 = a.is_first ? a.dist : a.d0;
+  *reinterpret_cast<double*>(out) = reward_calc(a.dist, d0, col, goal);
+  *reinterpret_cast<double*>(out + 8) = d0;
+  out[16] = col || goal;
+  out[17] = goal;
+  out[18] = col;
+}
+
 __global__ void footprint_kernel(ffmp_cfg_t cfg, int64_t n, const float* __restrict__ local_map,
                                  int64_t map_stride, uint8_t* collide) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2030,6 +2058,31 @@ int ffmp_reward_done_packed(const ffmp_cfg_t* cfg, void* host_buf, void* dev_buf
                 (long long)map_off, (long long)in_bytes);
   if (((uintptr_t)host_buf | (uintptr_t)dev_buf) & 15) return fail(FFMP_E_ARG, "ffmp_reward_done_packed: buffers must be 16-byte aligned");
   const hipStream_t s = (hipStream_t)stream;
+  if ((flags & 8) && !with_map && scan_len <= FFMP_PACKED_ARG_BEAMS) {
+    // inputs as kernel arguments, outputs into the pinned block itself: one launch and a synchronize
+    void* out_dev = nullptr;
+    if (hipHostGetDevicePointer(&out_dev, host_buf, 0) == hipSuccess && out_dev) {
+      if (int rc = check_cfg(cfg)) return rc;
+      const char* h = (const char*)host_buf;
+      PackedArgs a;
+      memcpy(a.scan, h + 48, 8 * (size_t)scan_len);
+      memcpy(&a.dist, h + 24, 8);
+      memcpy(&a.d0, h + 8, 8);
+      a.robot_r = cfg->robot_r;
+      a.goal_thr = cfg->goal_thr;
+      a.scan_len = scan_len;
+      a.is_first = (uint8_t)h[40];
+      a.collide_in = (uint8_t)h[41];
+      a.goal_in = (uint8_t)h[42];
+      a.flags = (uint8_t)(flags & 3);
+      hipLaunchKernelGGL(reward_done_args_kernel, dim3(1), dim3(64), 0, s, a, (uint8_t*)out_dev);
+      if (int rc = check_launch("ffmp_reward_done_packed")) return rc;
+      const hipError_t e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_reward_done_packed: %s", hipGetErrorString(e));
+      return FFMP_OK;
+    }
+    (void)hipGetLastError();  // not a mapped host block: the copies below
+  }
   if (hipMemcpyAsync(dev_buf, host_buf, (size_t)in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
     return fail(FFMP_E_HIP, "ffmp_reward_done_packed: host -> device copy failed");
   char* d = (char*)dev_buf;

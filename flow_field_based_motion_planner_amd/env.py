@@ -28,6 +28,7 @@ Every compute path goes through libffmp; without it (or without a GPU) calls rai
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 from typing import Optional
 
@@ -161,6 +162,10 @@ class FFMP(GymEnvBase):
             st = self._stage = (hin, torch.empty(cap, dtype=torch.uint8, device=self.device), hin.numpy())
         return st
 
+    # without a local map, ffmp_reward_done_packed's kernel-argument form (flag 8): no copies
+    # (FFMP_SINGLE_ARGS=0: the copy form, an A/B knob)
+    PACKED_ARGS = os.environ.get("FFMP_SINGLE_ARGS", "1") != "0"
+
     def _reward_done(self, rel_goal, is_first: bool, d0: float, scan=None, local_map=None,
                      collide_in=None, goal_in=None):
         lib = _abi.load()
@@ -189,6 +194,8 @@ class FFMP(GymEnvBase):
         if m is not None:
             hnp[moff:nbytes].view(np.float32).reshape(grid, grid)[:] = m
         flags = (0 if collide_in is None else 1) | (0 if goal_in is None else 2) | (0 if m is None else 4)
+        if m is None and L <= _abi.PACKED_ARG_BEAMS and self.PACKED_ARGS:
+            flags |= 8  # inputs as kernel arguments, outputs straight into the pinned block
         # one library call: the copy in, the kernel, the copy out, the stream synchronized
         _abi.check(lib.ffmp_reward_done_packed(C.byref(cfg_c), hin.data_ptr(), din.data_ptr(), nbytes, L, moff, grid,
                                                flags, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),

@@ -297,7 +297,11 @@ int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n,
  * is_first), done / is_goal / collide u8 @16, 17, 18; inputs rel_goal f64[2] @24, is_first /
  * collide_in / goal_in u8 @40, 41, 42, scan f64[scan_len] @48, the local map f32[map_grid^2] @map_off
  * (16-aligned, >= 48 + 8 scan_len).  flags: 1 = collide_in given, 2 = goal_in given, 4 = a local map
- * (cfg's footprint; cfg->grid need not equal map_grid). */
+ * (cfg's footprint; cfg->grid need not equal map_grid), 8 = without a map and with at most
+ * FFMP_PACKED_ARG_BEAMS beams, pass the inputs as kernel arguments and write the outputs straight
+ * into host_buf through its device view (hipHostGetDevicePointer: pinned, mapped memory) — one
+ * launch and a synchronize, no copies; host_buf not mapped: the copies as without the flag. */
+#define FFMP_PACKED_ARG_BEAMS 360
 int ffmp_reward_done_packed(const ffmp_cfg_t* cfg, void* host_buf, void* dev_buf, int64_t in_bytes, int32_t scan_len,
                             int64_t map_off, int32_t map_grid, int32_t flags, void* stream);
 

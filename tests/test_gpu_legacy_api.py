@@ -276,3 +276,38 @@ def test_footprint_cache_follows_the_attributes(ffmp):
     assert ffmp.is_collision(m) and len(ffmp.robot_grids) == 21
     r, done = ffmp.rewarder(m, np.array([3.0, 0.1]), True)
     assert done and r == -1.05
+
+
+def test_packed_kernel_argument_form_equals_copies(ffmp):
+    """ffmp_reward_done_packed flag 8 (inputs as kernel arguments, outputs straight into the pinned
+    block) against the copy form, bit for bit: random scans of 0 .. FFMP_PACKED_ARG_BEAMS beams with
+    zeros / NaN (None) / hits, is_first on and off, collide_in and goal_in given or not; more beams than
+    the argument block holds take the copy form."""
+    rng = np.random.default_rng(21)
+    cases = []
+    for L in (0, 1, 7, 180, 360, 361):
+        for _ in range(6):
+            scan = rng.uniform(0.0, 3.0, L)
+            if L:
+                scan[rng.random(L) < 0.2] = 0.0
+                scan[rng.random(L) < 0.05] = np.nan
+                if rng.random() < 0.3:
+                    scan[rng.integers(0, L)] = 0.05  # a hit
+            cases.append((scan, (float(rng.uniform(0, 5)), float(rng.uniform(-3, 3))), bool(rng.random() < 0.5),
+                          float(rng.uniform(0, 5)), [None, False, True][rng.integers(0, 3)],
+                          [None, False, True][rng.integers(0, 3)]))
+    old = envmod.FFMP.PACKED_ARGS
+    try:
+        outs = {}
+        for form in (True, False):
+            envmod.FFMP.PACKED_ARGS = form
+            outs[form] = [ffmp._reward_done(rg, first, d0, scan=sc, collide_in=ci, goal_in=gi)
+                          for sc, rg, first, d0, ci, gi in cases]
+    finally:
+        envmod.FFMP.PACKED_ARGS = old
+    for a, b in zip(outs[True], outs[False]):
+        assert a == b or (np.isnan(a[0]) and np.isnan(b[0]) and a[1:] == b[1:]), (a, b)
+    # the reference methods ride on it
+    with contextlib.redirect_stdout(io.StringIO()):  # is_collision2 prints the reference's banner
+        assert ffmp.is_collision2([None, 0.0, 0.05, 1.0])
+        assert not ffmp.is_collision2([None, 0.0, 0.5, 1.0])

@@ -105,6 +105,13 @@ def test_argument_validation_no_gpu(lib):
     assert lib.ffmp_raster(C.byref(flow_cfg), 0, p, None, C.byref(ob2), None) == 0
 
 
+def test_header_constants_match_the_binding():
+    import re
+    h = open(_abi.HEADER_PATH).read()
+    assert int(re.search(r"#define FFMP_PACKED_ARG_BEAMS (\d+)", h).group(1)) == _abi.PACKED_ARG_BEAMS
+    assert int(re.search(r"#define FFMP_ABI_VERSION (\d+)", h).group(1)) == _abi.ABI_VERSION
+
+
 def test_config_validation():
     with pytest.raises(ValueError):
         FFMPConfig(grid=66)

@@ -1498,7 +1498,13 @@ class StepGraph:
     for the raster of step i - 1 (the last reader of its buffer).  The graph's intermediate steps'
     small outputs (reward, done, state_g, ...) are overwritten one step early, which nobody sees: a
     replay's observation is its last step's, written in the same order as step() writes it, and the
-    frames, potential and record are bit-identical (tests/test_gpu_graph.py)."""
+    frames, potential and record are bit-identical (tests/test_gpu_graph.py).
+
+    Skewed (the default where skew_supported() and the one-off trial in _skew_pays() say it pays):
+    the same two record buffers, but the raster of step i and the env kernel of step i + 1 are ONE
+    launch (ffmp_step_skewed: env blocks first, raster blocks after), so a k-step replay is k + 1
+    dispatches on one stream instead of 2k and no env kernel waits on a raster tail.  Same results,
+    bit for bit (tests/test_gpu_graph.py, tests/timed_path_check.py)."""
 
     # Off by default: the overlap happens (rocprofv3 trace, profiles/r05n_pipelined_graph.txt) but the
     # raster beside an env kernel runs ~12 % longer and the graph leaves ~10 us between two rasters on

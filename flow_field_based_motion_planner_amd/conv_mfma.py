@@ -27,7 +27,7 @@ import torch
 
 from . import _abi
 
-CONV_RELU, CONV_OUT_BF16 = 1, 2  # include/ffmp.h FFMP_CONV_*
+CONV_RELU, CONV_OUT_BF16, CONV_W_FRAG = 1, 2, 4  # include/ffmp.h FFMP_CONV_*
 
 
 def _layer_ok(conv: torch.nn.Conv2d) -> bool:
@@ -66,6 +66,36 @@ def supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
     """torch's [N][C][KH][KW] weight -> the kernel's bf16 [KH][KW][N][C]."""
     return w.detach().to(torch.bfloat16).permute(2, 3, 0, 1).contiguous()
+
+
+def frag_order(wp: torch.Tensor) -> torch.Tensor:
+    """A plain packed weight [KH][KW][N][C] -> the kernels' fragment order [KH][KW][N/32][C/16][2][32][8]
+    (include/ffmp.h FFMP_CONV_W_FRAG: every 64-lane weight fragment load reads 1 KiB contiguous)."""
+    KH, KW, N, Cc = wp.shape
+    return wp.view(KH, KW, N // 32, 32, Cc // 16, 2, 8).permute(0, 1, 2, 4, 5, 3, 6).contiguous()
+
+
+def small_route(h: int, w: int, c: int, kh: int, kw: int, pad: int = 0, dx: int = 1) -> bool:
+    """Does ffmp_conv2d_fwd_bf16 run this shape on its small-image kernel (launch_fwd_wf's test,
+    csrc/ffmp_conv.hip)?  That kernel's weight loads are ~17 % of its time faster in fragment order
+    (profiles/r05sm_conv_small.txt); the row-ring kernel (conv2) gains nothing from it.  Only speed
+    rides on this: both kernels take either layout, with the same results bit for bit."""
+    ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - (kw - 1) * dx
+    if ho < 1 or wo < 1:
+        return False
+    cpr = 256 // (c * 2)  # lds_pitch / cell_off
+    pitch = (w - 1) * c * 2 + ((w - 1) // cpr) * 16 + c * 2
+    window = ((128 + wo - 1) // wo + 1 + kh - 1) * pitch + c * 2
+    return ho * wo <= 2048 and kh >= 4 and window <= 76 * 1024 and (w * c * 2) % 16 == 0
+
+
+def _fwd_weight(weight: torch.Tensor, kind: str, fn, h: int, w: int, c: int, kh: int, kw: int,
+                pad: int = 0) -> torch.Tensor:
+    """The cached kernel-layout weight for one forward launch: fragment order where the shape runs
+    on the small-image kernel, else the plain layout."""
+    if small_route(h, w, c, kh, kw, pad):
+        return packed(weight, kind + "_frag", lambda v: frag_order(fn(v)))
+    return packed(weight, kind, fn)
 
 
 def pack_weight_dgrad(w: torch.Tensor) -> torch.Tensor:
@@ -117,13 +147,21 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Te
                 out_dtype: torch.dtype = torch.float32, pad: int = 0, dx: int = 1) -> torch.Tensor:
     """y[b, yo, xo, n] = act(bias[n] + sum x[b, yo+ky, xo+kx*dx, c] w[ky, kx, n, c]) for an NHWC
     bf16 x [B, H, W, C] (zero-padded by `pad` cells on every side) and a packed weight
-    [KH, KW, N, C]; returns NHWC [B, H+2pad-KH+1, W+2pad-(KW-1)dx, N]."""
+    [KH, KW, N, C] (or the same in fragment order, frag_order's 7-d [KH, KW, N/32, C/16, 2, 32, 8]);
+    returns NHWC [B, H+2pad-KH+1, W+2pad-(KW-1)dx, N]."""
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("conv2d_nhwc takes bf16 x and packed weight")
     if not x.is_cuda or not x.is_contiguous() or not w_packed.is_contiguous():
         raise ValueError("conv2d_nhwc takes contiguous device tensors")
     B, H, W, Cin = x.shape
-    KH, KW, N, Cw = w_packed.shape
+    frag = w_packed.dim() == 7
+    if frag:
+        KH, KW, NB, S, two, r32, e8 = w_packed.shape
+        if (two, r32, e8) != (2, 32, 8):
+            raise ValueError(f"fragment-order weight must end in (2, 32, 8), got {tuple(w_packed.shape)}")
+        N, Cw = NB * 32, S * 16
+    else:
+        KH, KW, N, Cw = w_packed.shape
     if Cw != Cin:
         raise ValueError(f"channel mismatch: x has {Cin}, weight {Cw}")
     if out_dtype not in (torch.float32, torch.bfloat16):
@@ -132,7 +170,8 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Te
     b = None
     if bias is not None:
         b = bias.detach().to(device=x.device, dtype=torch.float32).contiguous()
-    flags = (CONV_RELU if relu else 0) | (CONV_OUT_BF16 if out_dtype == torch.bfloat16 else 0)
+    flags = (CONV_RELU if relu else 0) | (CONV_OUT_BF16 if out_dtype == torch.bfloat16 else 0) | \
+        (CONV_W_FRAG if frag else 0)
     lib = _abi.load()
     stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _abi.check(lib.ffmp_conv2d_fwd_bf16(x.data_ptr(), w_packed.data_ptr(), None if b is None else b.data_ptr(),
@@ -201,7 +240,8 @@ class MFMAConv2dReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
         xb = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # NHWC (free if x is channels-last)
-        wb = packed(weight, "fwd", pack_weight)
+        KH, KW = weight.shape[2], weight.shape[3]
+        wb = _fwd_weight(weight, "fwd", pack_weight, xb.shape[1], xb.shape[2], xb.shape[3], KH, KW)
         y = conv2d_nhwc(xb, wb, bias, relu=True, out_dtype=torch.bfloat16)
         ctx.save_for_backward(xb, weight, y)
         ctx.has_bias = bias is not None
@@ -220,8 +260,8 @@ class MFMAConv2dReLU(torch.autograd.Function):
             if dgrad_bm_ok(B, Hy, Wy, N, KH, KW, Cin):  # 32 samples per MFMA block: no zero products
                 gx = conv2d_dgrad_nhwc(g, packed(weight, "dgrad_bm", pack_weight_dgrad_bm))
             else:
-                gx = conv2d_nhwc(g, packed(weight, "dgrad", pack_weight_dgrad), None, out_dtype=torch.bfloat16,
-                                 pad=KH - 1)
+                wd = _fwd_weight(weight, "dgrad", pack_weight_dgrad, Hy, Wy, N, KH, KW, KH - 1)
+                gx = conv2d_nhwc(g, wd, None, out_dtype=torch.bfloat16, pad=KH - 1)
             gx = gx.permute(0, 3, 1, 2).to(ctx.x_dtype)
         if need[1]:  # on the matrix cores too: [KH][KW][N][C] -> torch's [N][C][KH][KW]
             gw = conv2d_wgrad_nhwc(g, xb, weight.shape[2], weight.shape[3]).permute(2, 3, 0, 1).to(weight.dtype)

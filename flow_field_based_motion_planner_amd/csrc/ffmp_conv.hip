@@ -81,6 +81,20 @@ __device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4
   }
 }
 
+// The B fragment of lane (r, h) for tap t, channel block nb, k-step s: 8 bf16 of weight row
+// n = nb * 32 + r, channels s * 16 + 8h .. +8.  WF = false: w [KH][KW][N][C] (the fragment's 64
+// lanes touch 32 rows 2 * C bytes apart, i.e. 32 cache lines for 1 KiB); WF = true
+// (FFMP_CONV_W_FRAG): w in fragment order [KH][KW][N / 32][C / 16][2][32][8], the 64 lanes read
+// 1 KiB contiguous — conv_small_kernel 0.48 -> 0.40 ms over the Network's conv3 / conv4 shapes at
+// B = 256, conv2's forward unchanged (profiles/r05sm_conv_small.txt, r05k_conv_fwd_probes.txt)
+template <int C, int NB, bool WF>
+__device__ __forceinline__ bf16x8 load_bfrag(const __bf16* __restrict__ w, int t, int nb, int s, int r, int h) {
+  if constexpr (WF)
+    return *(const bf16x8*)(w + (size_t)(((t * NB + nb) * (C / 16) + s) * 2 + h) * 256 + r * 8);
+  else
+    return *(const bf16x8*)(w + ((size_t)(t * NB * 32 + nb * 32 + r) * C + s * 16 + h * 8));
+}
+
 // Implicit zero padding of `pad` cells on every side: logical input rows/columns [pad, pad + H/W)
 // hold the tensor, the rest are zero.  A ring slot holds the W real cells of a row (zeros for a row
 // outside the tensor); with PAD, a lane whose logical column falls outside [pad, pad + W) reads a
@@ -104,7 +118,7 @@ __device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4
 #ifndef FFMP_CONV_FWD_OCC
 #define FFMP_CONV_FWD_OCC 2  // workgroups per CU the forward kernel is compiled for
 #endif
-template <int C, int NB, int MBW, bool PAD>
+template <int C, int NB, int MBW, bool PAD, bool WF>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
@@ -169,7 +183,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int s = 0; s < C / 16; ++s)
-        dst[nb][s] = *(const bf16x8*)(w + ((size_t)(t * N + nb * 32 + r) * C + s * 16 + h * 8));
+        dst[nb][s] = load_bfrag<C, NB, WF>(w, t, nb, s, r, h);
   };
   constexpr int kBAhead = FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
   bf16x8 bcur[NB][C / 16];
@@ -271,7 +285,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
 // instead (wave w takes kernel rows ky = w, w + 4, ...), each holding all 4 position blocks x NB
 // channel blocks; the input window of the tile (all its rows for every ky) is staged in LDS once,
 // and the 4 partial accumulators are summed through LDS in the epilogue.
-template <int C, int NB, bool PAD>
+template <int C, int NB, bool PAD, bool WF>
 __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                             const float* __restrict__ bias, void* __restrict__ y,
                                                             int H, int W, int KH, int KW, int pad, int dx, int flags) {
@@ -325,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int s = 0; s < C / 16; ++s)
-        bcur[nb][s] = *(const bf16x8*)(w + ((size_t)(ky * KW * N + nb * 32 + r) * C + s * 16 + h * 8));
+        bcur[nb][s] = load_bfrag<C, NB, WF>(w, ky * KW, nb, s, r, h);
     for (int kx = 0; kx < KW; ++kx) {
       const int tn = ky * KW + min(kx + 1, KW - 1);
       bf16x8 bnext[NB][C / 16];
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int s = 0; s < C / 16; ++s)
-          bnext[nb][s] = *(const bf16x8*)(w + ((size_t)(tn * N + nb * 32 + r) * C + s * 16 + h * 8));
+          bnext[nb][s] = load_bfrag<C, NB, WF>(w, tn, nb, s, r, h);
       int abase[MBW];
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
@@ -394,14 +408,14 @@ size_t small_window_bytes(int Wo, int KH, int W, int C) {
   return (size_t)((128 + Wo - 1) / Wo + 1 + KH - 1) * pitch + C * 2;  // + the zero column
 }
 
-template <int C, int NB, bool PAD>
+template <int C, int NB, bool PAD, bool WF>
 int launch_small(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
                  int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
   const dim3 grid((Ho * Wo + 127) / 128, B);
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w,
+  hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w,
                      bias, y, H, W, KH, KW, pad, dx, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
@@ -433,7 +447,7 @@ int pick_mbw(int P, int Wo, size_t slotbytes) {
   return 1;
 }
 
-template <int C, int NB, int MBW, bool PAD>
+template <int C, int NB, int MBW, bool PAD, bool WF>
 int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW,
                    int pad, int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
@@ -446,25 +460,32 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
+  hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
                      y, H, W, KH, KW, pad, dx, ring, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
   return FFMP_OK;
 }
 
-template <int C, int NB, bool PAD>
-int launch_fwd(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
+template <int C, int NB, bool PAD, bool WF>
+int launch_fwd_wf(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
                int dx, int flags, hipStream_t s) {
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   // small images with a kernel deep enough to split over the waves: conv_small_kernel
   if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= 76 * 1024 && (W * C * 2) % 16 == 0)
-    return launch_small<C, NB, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    return launch_small<C, NB, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
   switch (pick_mbw(Ho * Wo, Wo, (size_t)lds_pitch<C>(W))) {
-    case 4: return launch_fwd_mbw<C, NB, 4, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-    case 2: return launch_fwd_mbw<C, NB, 2, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-    default: return launch_fwd_mbw<C, NB, 1, PAD>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    case 4: return launch_fwd_mbw<C, NB, 4, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    case 2: return launch_fwd_mbw<C, NB, 2, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    default: return launch_fwd_mbw<C, NB, 1, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
   }
+}
+
+template <int C, int NB, bool PAD>
+int launch_fwd(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
+               int dx, int flags, hipStream_t s) {
+  if (flags & FFMP_CONV_W_FRAG) return launch_fwd_wf<C, NB, PAD, true>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+  return launch_fwd_wf<C, NB, PAD, false>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -909,6 +930,8 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
     return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: bad shape (batch %d, %d x %d input, %d x %d kernel, pad %d, dx %d)",
                 batch, h, wd, kh, kw, pad, dx);
   if (((uintptr_t)x | (uintptr_t)w) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: x and w must be 16-byte aligned");
+  if (flags & ~(FFMP_CONV_RELU | FFMP_CONV_OUT_BF16 | FFMP_CONV_W_FRAG))
+    return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: unknown flags 0x%x", flags);
   hipStream_t s = (hipStream_t)stream;
   if (pad > 0) {  // data gradients of the 32/64-channel convolutions (c = their output channels)
     if (c == 64 && n == 32) return launch_fwd<64, 1, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);

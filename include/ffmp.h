@@ -334,9 +334,15 @@ int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits,
  * accumulation on v_mfma_f32_32x32x16_bf16 (products exact, sums in fp32).  x and w 16-byte
  * aligned.  With pad = k - 1 and the kernel flipped and transposed (w'[ky][kx][c][n] =
  * w[k-1-ky][k-1-kx][n][c]) it is the data gradient of the unpadded convolution.
+ * FFMP_CONV_W_FRAG: w holds the same elements in the kernels' fragment order,
+ * [kh][kw][n/32][c/16][2][32][8] — weight (ky, kx, output channel o, input channel i) at index
+ * ((((ky*kw + kx)*(n/32) + o/32)*(c/16) + i/16)*2 + (i%16)/8)*256 + (o%32)*8 + i%8 — so that each
+ * 64-lane weight fragment load reads 1 KiB contiguous (the small-image kernel of conv3 / conv4:
+ * ~17 % faster); the results are bit-identical to the plain layout's.
  * Returns FFMP_OK or a negative code (ffmp_last_error()). */
 #define FFMP_CONV_RELU 1
 #define FFMP_CONV_OUT_BF16 2
+#define FFMP_CONV_W_FRAG 4
 int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* y, int32_t batch, int32_t h,
                          int32_t wd, int32_t c, int32_t kh, int32_t kw, int32_t n, int32_t pad, int32_t dx,
                          int32_t flags, void* stream);

@@ -53,3 +53,27 @@ def test_relu_backward_matches_mask_multiply():
     # an fp32 incoming gradient is rounded to bf16 first, as before
     g32 = conv_mfma.relu_masked_nhwc(gy.float(), y)
     assert torch.equal(g32, ref)
+
+
+def test_frag_order_matches_the_header_index():
+    """conv_mfma.frag_order puts weight (ky, kx, o, i) where include/ffmp.h's FFMP_CONV_W_FRAG says."""
+    KH, KW, N, Cc = 2, 3, 64, 32
+    wp = torch.arange(KH * KW * N * Cc, dtype=torch.float32).view(KH, KW, N, Cc)
+    flat = conv_mfma.frag_order(wp).flatten()
+    assert flat.shape == wp.flatten().shape
+    for ky, kx, o, i in [(0, 0, 0, 0), (1, 2, 63, 31), (0, 1, 33, 9), (1, 0, 5, 17), (1, 1, 40, 24)]:
+        idx = ((((ky * KW + kx) * (N // 32) + o // 32) * (Cc // 16) + i // 16) * 2 + (i % 16) // 8) * 256 \
+            + (o % 32) * 8 + i % 8
+        assert flat[idx] == wp[ky, kx, o, i]
+
+
+def test_small_route_mirrors_the_library_shapes():
+    """The Network's conv3 / conv4 forwards and their data gradients run on the small-image kernel
+    (fragment-order weights); conv2 and its transposed form on the row-ring kernel."""
+    for h in (38, 31, 24, 17):
+        assert conv_mfma.small_route(h, h, 64, 8, 8)
+    for hy in (31, 24, 17, 10):
+        assert conv_mfma.small_route(hy, hy, 64, 8, 8, pad=7)
+    assert not conv_mfma.small_route(69, 69, 32, 32, 32)       # conv2
+    assert not conv_mfma.small_route(38, 38, 64, 32, 32, 31)   # conv2's transposed form
+    assert not conv_mfma.small_route(100, 69, 32, 32, 2, 0, 16)  # the folded conv1

@@ -11,7 +11,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from flow_field_based_motion_planner_amd.conv_mfma import MFMAConv2dReLU, conv2d_nhwc, pack_weight
+from flow_field_based_motion_planner_amd.conv_mfma import MFMAConv2dReLU, conv2d_nhwc, frag_order, pack_weight
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -54,6 +54,10 @@ def test_conv_fwd_matches_float64(B, H, W, C, K, N, pad):
     # fused ReLU + bf16 output: the same fp32 accumulator, rounded
     yb = conv2d_nhwc(xb, wp, bias, relu=True, out_dtype=torch.bfloat16, pad=pad)
     assert torch.equal(yb, torch.relu(y).to(torch.bfloat16))
+    # the weight in fragment order (FFMP_CONV_W_FRAG): the same products in the same order, bit for bit
+    wf = frag_order(wp)
+    assert torch.equal(conv2d_nhwc(xb, wf, bias, pad=pad), y)
+    assert torch.equal(conv2d_nhwc(xb, wf, bias, relu=True, out_dtype=torch.bfloat16, pad=pad), yb)
 
 
 @pytest.mark.parametrize("B,C,H,N,K", [(4, 32, 69, 64, 32),   # conv2
@@ -131,6 +135,7 @@ def test_conv_dilated_matches_float64(B, H, W, KH, KW, dx, N):
         absref = F.conv2d(x64.abs(), w64.abs(), dilation=(1, dx)).permute(0, 2, 3, 1)
     assert y.shape == ref.shape
     assert not bool(((y.double() - ref).abs() > 5e-5 * absref + 1e-6).any())
+    assert torch.equal(conv2d_nhwc(xb, frag_order(pack_weight(w)), None, dx=dx), y)  # FFMP_CONV_W_FRAG
 
 
 @pytest.mark.parametrize("C", [2, 1, 3, 12])

@@ -333,9 +333,9 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
         F = 32 // x.shape[1]
-        y = conv2d_nhwc(fold_input(x, F), packed(weight, f"fold{F}", lambda v: pack_weight_fold(v, F)), bias,
-                        relu=True, out_dtype=torch.bfloat16,
-                        dx=F)
+        # fragment-order weights: 0-3 % faster at B = 256 (profiles/r05fab_conv_frag_ab.txt, r05sf_learner.txt)
+        wf = packed(weight, f"fold{F}_frag", lambda v: frag_order(pack_weight_fold(v, F)))
+        y = conv2d_nhwc(fold_input(x, F), wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
         ctx.save_for_backward(x, weight, y)
         ctx.has_bias = bias is not None
         return y.permute(0, 3, 1, 2)

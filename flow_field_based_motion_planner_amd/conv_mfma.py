@@ -27,7 +27,7 @@ import torch
 
 from . import _abi
 
-CONV_RELU, CONV_OUT_BF16, CONV_W_FRAG = 1, 2, 4  # include/ffmp.h FFMP_CONV_*
+CONV_RELU, CONV_OUT_BF16, CONV_W_FRAG, CONV_X_FOLD = 1, 2, 4, 8  # include/ffmp.h FFMP_CONV_*
 
 
 def _layer_ok(conv: torch.nn.Conv2d) -> bool:
@@ -144,16 +144,19 @@ def dgrad_bm_ok(batch: int, hy: int, wy: int, c: int, kh: int, kw: int, n: int) 
 
 
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
-                out_dtype: torch.dtype = torch.float32, pad: int = 0, dx: int = 1) -> torch.Tensor:
+                out_dtype: torch.dtype = torch.float32, pad: int = 0, dx: int = 1, x_fold: bool = False) -> torch.Tensor:
     """y[b, yo, xo, n] = act(bias[n] + sum x[b, yo+ky, xo+kx*dx, c] w[ky, kx, n, c]) for an NHWC
     bf16 x [B, H, W, C] (zero-padded by `pad` cells on every side) and a packed weight
     [KH, KW, N, C] (or the same in fragment order, frag_order's 7-d [KH, KW, N/32, C/16, 2, 32, 8]);
-    returns NHWC [B, H+2pad-KH+1, W+2pad-(KW-1)dx, N]."""
+    returns NHWC [B, H+2pad-KH+1, W+2pad-(KW-1)dx, N].  x_fold: x is the unfolded [B, H, W + dx - 1,
+    C / dx] input whose fold_input(., dx) the kernel reads on the fly (FFMP_CONV_X_FOLD)."""
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("conv2d_nhwc takes bf16 x and packed weight")
     if not x.is_cuda or not x.is_contiguous() or not w_packed.is_contiguous():
         raise ValueError("conv2d_nhwc takes contiguous device tensors")
     B, H, W, Cin = x.shape
+    if x_fold:  # the folded image the kernel sees
+        W, Cin = W - dx + 1, Cin * dx
     frag = w_packed.dim() == 7
     if frag:
         KH, KW, NB, S, two, r32, e8 = w_packed.shape
@@ -171,7 +174,7 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Te
     if bias is not None:
         b = bias.detach().to(device=x.device, dtype=torch.float32).contiguous()
     flags = (CONV_RELU if relu else 0) | (CONV_OUT_BF16 if out_dtype == torch.bfloat16 else 0) | \
-        (CONV_W_FRAG if frag else 0)
+        (CONV_W_FRAG if frag else 0) | (CONV_X_FOLD if x_fold else 0)
     lib = _abi.load()
     stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _abi.check(lib.ffmp_conv2d_fwd_bf16(x.data_ptr(), w_packed.data_ptr(), None if b is None else b.data_ptr(),
@@ -335,7 +338,11 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
         F = 32 // x.shape[1]
         # fragment-order weights: 0-3 % faster at B = 256 (profiles/r05fab_conv_frag_ab.txt, r05sf_learner.txt)
         wf = packed(weight, f"fold{F}_frag", lambda v: frag_order(pack_weight_fold(v, F)))
-        y = conv2d_nhwc(fold_input(x, F), wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
+        if x.shape[1] % 2 == 0:  # the kernel folds the NHWC input on the fly (dword cells: >= 2 channels)
+            xn = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+            y = conv2d_nhwc(xn, wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F, x_fold=True)
+        else:
+            y = conv2d_nhwc(fold_input(x, F), wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
         ctx.save_for_backward(x, weight, y)
         ctx.has_bias = bias is not None
         return y.permute(0, 3, 1, 2)

@@ -46,13 +46,33 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 4;
 
+// One input row's 16-byte chunks into registers.  cellb = bytes between two cells of the row in
+// global memory: C * 2 (a plain NHWC row), or, for an input folded on the fly (FFMP_CONV_X_FOLD),
+// the unfolded cell's (C / F) * 2 — folded cell x is then the C * 2 bytes starting at unfolded cell
+// x (dword-aligned, read as dwords).
 template <int C>
-__device__ __forceinline__ void load_row_regs(const char* __restrict__ src, int chunks, uint4 (&buf)[4]) {
+__device__ __forceinline__ void load_row_regs(const char* __restrict__ src, int chunks, int cellb, uint4 (&buf)[4]) {
+  constexpr int CPC = C / 8;  // 16-byte chunks per cell
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = threadIdx.x + 256 * i;
-    if (q < chunks) buf[i] = src ? *(const uint4*)(src + 16 * (size_t)q) : uint4{0u, 0u, 0u, 0u};
+    if (q >= chunks) continue;
+    if (!src) {
+      buf[i] = uint4{0u, 0u, 0u, 0u};
+    } else if (cellb == C * 2) {
+      buf[i] = *(const uint4*)(src + 16 * (size_t)q);
+    } else {
+      const uint32_t* p = (const uint32_t*)(src + (size_t)(q / CPC) * cellb + 16 * (q % CPC));
+      buf[i] = uint4{p[0], p[1], p[2], p[3]};
+    }
   }
+}
+
+// global geometry of the input rows: cell bytes and row bytes (see load_row_regs)
+template <int C>
+__device__ __forceinline__ int2 in_geom(int W, int dx, int flags) {
+  if (flags & FFMP_CONV_X_FOLD) return int2{(C / dx) * 2, (W + dx - 1) * (C / dx) * 2};
+  return int2{C * 2, W * C * 2};
 }
 
 // LDS images of NHWC rows are padded by 16 bytes after every 256: column col starts at
@@ -131,13 +151,14 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   const int p0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int rowbytes = W * C * 2;      // one tensor row
+  const int rowbytes = W * C * 2;      // one tensor row (of the folded image with FFMP_CONV_X_FOLD)
   const int pitch = lds_pitch<C>(W);   // its padded image = one ring slot
   const int chunks = rowbytes / 16;    // <= 4 * 256 (host check)
+  const int2 gin = in_geom<C>(W, dx, flags);  // the row's cell / row bytes in global memory
   const int zero_off = RING * pitch;   // a zero column (PAD: reads outside the tensor's columns)
   const int yf = p0 / Wo;
   const int yl = min(P - 1, p0 + PT - 1) / Wo;
-  const char* xb = (const char*)x + (size_t)b * H * rowbytes;
+  const char* xb = (const char*)x + (size_t)b * H * gin.y;
   // kernel rows whose input rows [yf + ky, yl + ky] meet the tensor rows [pad, pad + H) ...
   const int ky_lo = max(0, pad - yl), ky_hi = min(KH - 1, pad + H - 1 - yf);
   // ... and this wave's share of them (its positions' rows)
@@ -156,12 +177,12 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   }
   auto row_src = [&](int yr) -> const char* {  // logical row -> tensor row, or nullptr (zeros)
     const int real = yr - pad;
-    return (real >= 0 && real < H) ? xb + (size_t)real * rowbytes : nullptr;
+    return (real >= 0 && real < H) ? xb + (size_t)real * gin.y : nullptr;
   };
   // ring rows for the first kernel row
   for (int row = yf + ky_lo; row <= yl + ky_lo; ++row) {
     uint4 buf[4];
-    load_row_regs<C>(row_src(row), chunks, buf);
+    load_row_regs<C>(row_src(row), chunks, gin.x, buf);
     store_row_lds<C>(lds + (row % RING) * pitch, chunks, buf);
   }
   if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
@@ -193,7 +214,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   for (int ky = ky_lo; ky <= ky_hi; ++ky) {
     uint4 nrow[4];
     const bool more = ky < ky_hi;
-    if (more) load_row_regs<C>(row_src(yl + ky + 1), chunks, nrow);
+    if (more) load_row_regs<C>(row_src(yl + ky + 1), chunks, gin.x, nrow);
     if (ky >= wk_lo && ky <= wk_hi) {
       int aoff[MBW];
 #pragma unroll
@@ -299,20 +320,23 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
   const int r = lane & 31, h = lane >> 5;
   const int rowbytes = W * C * 2;
   const int pitch = lds_pitch<C>(W);  // padded row images (cell_off)
+  const int2 gin = in_geom<C>(W, dx, flags);
   const int chunks = rowbytes / 16;
   const int yf = p0 / Wo;
   const int yl = min(P - 1, p0 + PT - 1) / Wo;
-  const char* xb = (const char*)x + (size_t)b * H * rowbytes;
+  const char* xb = (const char*)x + (size_t)b * H * gin.y;
   const int ky_lo = max(0, pad - yl), ky_hi = min(KH - 1, pad + H - 1 - yf);
   const int zero_off = (yl + ky_hi - yf - ky_lo + 1) * pitch;  // a zero column after the window
 
   // the window: logical rows [yf + ky_lo, yl + ky_hi], slot = row - yf - ky_lo
   for (int row = yf + ky_lo; row <= yl + ky_hi; ++row) {
     const int real = row - pad;
-    const char* src = (real >= 0 && real < H) ? xb + (size_t)real * rowbytes : nullptr;
-    for (int q = threadIdx.x; q < chunks; q += 256)
-      *(uint4*)(lds + (row - yf - ky_lo) * pitch + cell_off<C>(q / (C / 8)) + 16 * (q % (C / 8))) =
-          src ? *(const uint4*)(src + 16 * (size_t)q) : uint4{0u, 0u, 0u, 0u};
+    const char* src = (real >= 0 && real < H) ? xb + (size_t)real * gin.y : nullptr;
+    for (int q0 = 0; q0 < chunks; q0 += 1024) {
+      uint4 buf[4];
+      load_row_regs<C>(src ? src + (size_t)(q0 / (C / 8)) * gin.x : nullptr, chunks - q0, gin.x, buf);
+      store_row_lds<C>(lds + (row - yf - ky_lo) * pitch + cell_off<C>(q0 / (C / 8)), chunks - q0, buf);
+    }
   }
   if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
   int ypos[MBW], xcol[MBW];
@@ -930,8 +954,11 @@ int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* 
     return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: bad shape (batch %d, %d x %d input, %d x %d kernel, pad %d, dx %d)",
                 batch, h, wd, kh, kw, pad, dx);
   if (((uintptr_t)x | (uintptr_t)w) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: x and w must be 16-byte aligned");
-  if (flags & ~(FFMP_CONV_RELU | FFMP_CONV_OUT_BF16 | FFMP_CONV_W_FRAG))
+  if (flags & ~(FFMP_CONV_RELU | FFMP_CONV_OUT_BF16 | FFMP_CONV_W_FRAG | FFMP_CONV_X_FOLD))
     return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: unknown flags 0x%x", flags);
+  if ((flags & FFMP_CONV_X_FOLD) && (dx < 2 || c % dx || ((c / dx) * 2) % 4 || pad))
+    return fail(FFMP_E_ARG, "ffmp_conv2d_fwd_bf16: FFMP_CONV_X_FOLD needs dx >= 2 dividing c into an even channel count "
+                "and pad 0 (got c %d, dx %d, pad %d)", c, dx, pad);
   hipStream_t s = (hipStream_t)stream;
   if (pad > 0) {  // data gradients of the 32/64-channel convolutions (c = their output channels)
     if (c == 64 && n == 32) return launch_fwd<64, 1, true>(x, w, bias, y, batch, h, wd, kh, kw, pad, dx, flags, s);

@@ -339,10 +339,15 @@ int ffmp_check_exact_math(int32_t which, uint32_t lo_bits, uint32_t hi_bits,
  * ((((ky*kw + kx)*(n/32) + o/32)*(c/16) + i/16)*2 + (i%16)/8)*256 + (o%32)*8 + i%8 — so that each
  * 64-lane weight fragment load reads 1 KiB contiguous (the small-image kernel of conv3 / conv4:
  * ~17 % faster); the results are bit-identical to the plain layout's.
+ * FFMP_CONV_X_FOLD (pad 0, dx = F >= 2 dividing c into an even count c / F): x is the UNFOLDED
+ * NHWC input [batch][h][wd+F-1][c/F] of a few-channel convolution whose F consecutive kernel
+ * columns were folded into channels; the kernel reads the folded image x'[b][y][x][j*(c/F) + i] =
+ * x[b][y][x+j][i] — c / F <= 16 channels, wd columns — from it directly (no materialized fold).
  * Returns FFMP_OK or a negative code (ffmp_last_error()). */
 #define FFMP_CONV_RELU 1
 #define FFMP_CONV_OUT_BF16 2
 #define FFMP_CONV_W_FRAG 4
+#define FFMP_CONV_X_FOLD 8
 int ffmp_conv2d_fwd_bf16(const void* x, const void* w, const float* bias, void* y, int32_t batch, int32_t h,
                          int32_t wd, int32_t c, int32_t kh, int32_t kw, int32_t n, int32_t pad, int32_t dx,
                          int32_t flags, void* stream);

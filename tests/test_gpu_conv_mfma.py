@@ -231,3 +231,23 @@ def test_dgrad_samples_as_m_shape_limits():
     assert not dgrad_bm_ok(256, 31, 31, 64, 8, 8, 64)   # conv3's: 64 output channels
     assert not dgrad_bm_ok(2, 5, 10, 64, 3, 64, 32)     # output rows of 73 positions
     assert not dgrad_bm_ok(2, 10, 41, 64, 3, 3, 32)     # 41 columns x 2 KiB x 2 rows > 160 KiB
+
+
+@pytest.mark.parametrize("Cc", [2, 4, 16])
+@pytest.mark.parametrize("wide", [False, True])  # the small-image kernel / the row-ring kernel
+def test_conv_x_fold_equals_materialized_fold(Cc, wide):
+    """FFMP_CONV_X_FOLD: the kernel folding the unfolded NHWC input on the fly == the same launch on
+    fold_input's materialized copy, bit for bit (plain and fragment-order weights)."""
+    from flow_field_based_motion_planner_amd.conv_mfma import fold_input, pack_weight_fold, small_route
+    F = 32 // Cc
+    g = torch.Generator(device=DEV).manual_seed(Cc)
+    x = torch.randn((3, Cc, 45, 100 if wide else 37 + F), device=DEV, generator=g)
+    assert small_route(45, x.shape[3] - F + 1, 32, 5, 2, 0, F) != wide
+    w = torch.randn((32, Cc, 5, 2 * F), device=DEV, generator=g) / (Cc * 10 * F) ** 0.5
+    bias = torch.randn(32, device=DEV, generator=g)
+    wp = pack_weight_fold(w, F)
+    xn = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+    for wk in (wp, frag_order(wp)):
+        ref = conv2d_nhwc(fold_input(x, F), wk, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
+        got = conv2d_nhwc(xn, wk, bias, relu=True, out_dtype=torch.bfloat16, dx=F, x_fold=True)
+        assert got.shape == ref.shape and torch.equal(got, ref)

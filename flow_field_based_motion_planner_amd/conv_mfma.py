@@ -311,10 +311,17 @@ def fold_supported(conv: torch.nn.Conv2d, x_shape=None) -> bool:
             and shape_ok(1, B, H, W - F + 1, 32, KH, KW // F, conv.out_channels, 0, F))
 
 
+def nhwc_bf16(x: torch.Tensor) -> torch.Tensor:
+    """x (B, C, H, W), any dtype / strides -> a contiguous bf16 NHWC copy, in one kernel (cast and
+    transpose together)."""
+    B, Cc, H, W = x.shape
+    return torch.empty((B, H, W, Cc), dtype=torch.bfloat16, device=x.device).copy_(x.permute(0, 2, 3, 1))
+
+
 def fold_input(x: torch.Tensor, F: int) -> torch.Tensor:
     """x (B, C, H, W) -> bf16 NHWC (B, H, W - F + 1, F * C) with channel j*C + c = x[:, c, :, x + j]."""
     B, Cc, H, W = x.shape
-    xn = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # (B, H, W, C)
+    xn = nhwc_bf16(x)  # (B, H, W, C)
     s = xn.stride()
     v = xn.as_strided((B, H, W - F + 1, F, Cc), (s[0], s[1], s[2], s[2], s[3]))
     return v.reshape(B, H, W - F + 1, F * Cc).contiguous()
@@ -339,8 +346,7 @@ class MFMAFoldConv2dReLU(torch.autograd.Function):
         # fragment-order weights: 0-3 % faster at B = 256 (profiles/r05fab_conv_frag_ab.txt, r05sf_learner.txt)
         wf = packed(weight, f"fold{F}_frag", lambda v: frag_order(pack_weight_fold(v, F)))
         if x.shape[1] % 2 == 0:  # the kernel folds the NHWC input on the fly (dword cells: >= 2 channels)
-            xn = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
-            y = conv2d_nhwc(xn, wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F, x_fold=True)
+            y = conv2d_nhwc(nhwc_bf16(x), wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F, x_fold=True)
         else:
             y = conv2d_nhwc(fold_input(x, F), wf, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
         ctx.save_for_backward(x, weight, y)

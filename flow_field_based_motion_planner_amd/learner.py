@@ -92,7 +92,10 @@ class Brain:
         if self.channels_last:  # NHWC convolutions (same values; MIOpen picks other kernels)
             self.main_q_network.to(memory_format=torch.channels_last)
             self.target_q_network.to(memory_format=torch.channels_last)
-        self.optimizer = torch.optim.Adam(self.main_q_network.parameters(), lr=lr)
+        # torch's fused Adam on the GPU: one kernel per step instead of the foreach chain (~7 launches,
+        # ~0.15 ms per update at the reference's Network), the same update up to fp32 rounding
+        self.optimizer = torch.optim.Adam(self.main_q_network.parameters(), lr=lr,
+                                          fused=self.device.type == "cuda")
         self.loss: Optional[torch.Tensor] = None
         self.step = 0
         self.gen = torch.Generator(device=self.device)

@@ -59,7 +59,10 @@ def test_default_c3_parks_no_hbm():
     grew, held = free0 - free1, env.hbm_bytes()
     assert env.ring == "seamless" and env.frame_window == 8
     assert grew - held <= 0.10 * held, (grew, held, env.ring_meta)
-    assert env._ring.info()["pieces_new"] >= 64  # it did pair (and may have probed extra pieces)
+    # it did pair: the first 12 positions are always probed (ffmp_ring.hip choose_pieces).  Not
+    # pieces_new >= 64: a ring an earlier test in this process dropped without close() may still be
+    # retired here, and its pieces are legitimately reused as candidates (seen once: 21 new of 64)
+    assert env._ring.info()["pair_probes"] >= 12
     env.reset()
     env.step(torch.zeros(32768, dtype=torch.int64, device="cuda:0"))
     env.close()

@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--envs", type=int, default=0, help="override envs per rank")
+    p.add_argument("--env-offset", type=int, default=None,
+                   help="global index of this rank's first env (default rank x envs); e.g. --config C4 --envs 8192 "
+                        "--env-offset 57344 runs the 8-GPU strong leg's rank-7 shard on one GPU")
     p.add_argument("--no-potential", action="store_true")
     p.add_argument("--flow", action="store_true", help="also raster the BEV motion-flow planes (not a BASELINE config)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (0 = skip)")
@@ -76,6 +79,9 @@ def parse():
                    help="with --graph on: replay graphs whose steps are ONE launch each (the raster of step i + the "
                         "env step of step i + 1, ffmp_step_skewed) — auto: time both graphs (3 alternating replays "
                         "each, untimed) and keep the faster; on / off: force")
+    p.add_argument("--closed-loop", type=int, default=1,
+                   help="1 (default): after the open-loop timing, time the main leg closed-loop too (each step's "
+                        "actions computed on the device from the previous observation: `closed_loop`); 0: skip")
     p.add_argument("--save-tuning", default=None, help="write the instance's launch choices (JSON) here")
     p.add_argument("--tuning", default=None,
                    help="launch choices from --save-tuning instead of the autotune (profiling runs: only timed "
@@ -492,6 +498,9 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     kernel_ms = (sum(r_ms[:K // per]) / (K // per)) if graph is not None else sum(r_ms) / len(r_ms)
     per_rank = _gather_floats(rank_record(el_local, construct_s, n, kernel_ms, achieved / PEAK_HBM_GBS, env),
                               world, dev, args.dist_backend)
+    closed = None
+    if main_leg and args.closed_loop and env.pipeline_slices == 1:
+        closed = closed_loop_leg(env, K, W, world, dev, args.dist_backend, b["total"])
     el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
     n_total = int(sum(r[2] for r in per_rank))
     out = {
@@ -526,8 +535,75 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
         "raster_autotune": env.placement,
         "hbm_roofline_pct_whole_step": 100.0 * (b["total"] * n_total * K / el / 1e9) / (PEAK_HBM_GBS * world),
         "per_launch_envs": raster_ev[0][2],
+        "closed_loop": closed,
     }
+    if closed is not None:
+        for k in ("step_graph", "step_plain", "policy_graph"):
+            closed[k]["vs_open_loop"] = closed[k]["value"] / out["value"]
     return out, env
+
+
+def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_bytes: float) -> dict:
+    """Closed loop (src/train.py:572-577, 665-682: each action is chosen from the previous
+    observation, never known a step ahead): step k + 1's actions come from step k's observation on
+    the device (FFMPVec.policy_reactive, include/ffmp.h ffmp_policy_reactive: reads state_g and the
+    newest frame) inside the timed region.  Three forms, K steps each, max over ranks:
+      step_graph   the per-step API — policy_reactive into action_buffer, then step() replaying a
+                   single-step HIP graph (FFMPVec.use_graphs);
+      step_plain   the same loop with plain launches;
+      policy_graph the policy captured inside a graph of graph_period() steps (capture(policy=...)),
+                   replayed with no host work between steps (the K % period rest: step_graph steps)."""
+    import torch
+    import torch.distributed as dist
+    n = env.num_envs
+    out = {"policy": "ffmp_policy_reactive (scripted controller; reads state_g and the newest frame)",
+           "steps": K}
+
+    def timed(body):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        body()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    def step_loop(k):
+        for _ in range(k):
+            env.step(env.policy_reactive(out=env.action_buffer))
+
+    env.use_graphs(True)
+    step_loop(max(warm, env.graph_period() + 1))  # every ring position's graph captured and warm
+    el = {"step_graph": timed(lambda: step_loop(K))}
+    env.use_graphs(False)
+    step_loop(warm)
+    el["step_plain"] = timed(lambda: step_loop(K))
+    env.use_graphs(True)
+    per = env.graph_period()
+    pg = env.capture(policy="reactive")
+    pg.replay()
+    rem = K % pg.steps
+    torch.cuda.synchronize()
+
+    def graph_loop():
+        for _ in range(K // pg.steps):
+            pg.replay()
+        step_loop(rem)
+    el["policy_graph"] = timed(graph_loop)
+    env.use_graphs(False)
+    keys = ("step_graph", "step_plain", "policy_graph")
+    rows = _gather_floats([el[k] for k in keys], world, dev, backend)
+    for i, k in enumerate(keys):
+        t = max(r[i] for r in rows)
+        rate = n * world * K / t  # equal shards: every rank steps n envs
+        out[k] = {"value": rate, "unit": "env-steps/s", "ms_per_step": t * 1e3 / K,
+                  "hbm_roofline_pct_whole_step": 100.0 * step_bytes * rate / 1e9 / (PEAK_HBM_GBS * world)}
+    out["policy_graph"]["steps_per_replay"] = pg.steps
+    out["graph_period"] = per
+    env.check_errors()
+    return out
 
 
 def _release(env):
@@ -635,7 +711,8 @@ def main():
     name = args.config
     cfg, n, strong = _leg_size(name, args, world, dev)
     K, W = args.steps, args.warmup
-    leg, env = run_leg(args, name, cfg, n, rank * n, K, W, dev, world, rank, strong, True)
+    off0 = rank * n if args.env_offset is None else args.env_offset + rank * n
+    leg, env = run_leg(args, name, cfg, n, off0, K, W, dev, world, rank, strong, True)
     traffic, traffic_source = load_traffic(name, leg["per_launch_envs"], env.frame_window, env.ring, env.fused,
                                            args.obs_format, (leg["graph"] or {}).get("steps_per_replay", 0),
                                            bool((leg["graph"] or {}).get("skewed", False)))
@@ -686,7 +763,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if args.obs_format == "f32" else "u8 frames / f16 potential (f32 compute)",
             "data": "synthetic",
-            "config": {"workload": name, "n_envs_total": leg["n_envs_total"], "n_envs_per_gpu": n, "grid": cfg.grid,
+            "config": {"workload": name, "n_envs_total": leg["n_envs_total"], "n_envs_per_gpu": n, "env_offset": off0,
+                       "grid": cfg.grid,
                        "n_obst": cfg.n_obst, "moving": bool(cfg.moving), "n_beams": cfg.n_beams,
                        "potential": not args.no_potential, "flow": bool(args.flow), "obs_format": args.obs_format,
                        "frame_window": leg["frame_window"], "ring": leg["ring"], "fused": leg["fused"],
@@ -713,6 +791,8 @@ def main():
             "raster_autotune": leg["raster_autotune"],
             "hbm_roofline_pct_whole_step": leg["hbm_roofline_pct_whole_step"],
         }
+        if leg.get("closed_loop") is not None:
+            out["closed_loop"] = leg["closed_loop"]
         if strong_leg is not None:
             out["strong"] = strong_leg
         if compact is not None:

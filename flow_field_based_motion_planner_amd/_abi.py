@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFMP_LIB", os.path.join(_HERE, "lib", "libffmp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ffmp.h")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 OBS_F32, OBS_U8F16 = 0, 1  # include/ffmp.h FFMP_OBS_*
 MAX_SERIES = 16  # FFMP_MAX_SERIES (ffmp_temporal_maps)
 PACKED_ARG_BEAMS = 360  # FFMP_PACKED_ARG_BEAMS (ffmp_reward_done_packed flag 8)
@@ -110,6 +110,8 @@ _SIGS = {
                                   C.POINTER(OutT), _I32, _P]),
     "ffmp_step_skewed": (C.c_int, [C.POINTER(CfgT), _I64, _I64, _P, C.POINTER(StateT), C.POINTER(ObsT),
                                    C.POINTER(OutT), _P, _I32, _I32, _P]),
+    "ffmp_step_skewed_check": (C.c_int, [C.POINTER(CfgT), _I32, _I32]),
+    "ffmp_policy_reactive": (C.c_int, [C.POINTER(CfgT), _I64, C.POINTER(ObsT), _P, _P]),
     "ffmp_reward_done": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P]),
     "ffmp_footprint_collision": (C.c_int, [C.POINTER(CfgT), _I64, _P, _I64, _P, _P]),

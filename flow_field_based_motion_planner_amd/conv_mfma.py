@@ -205,11 +205,27 @@ def conv2d_wgrad_nhwc(g: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dx: in
     return part.sum(0) if chunks > 1 else part[0]
 
 
+def _bump_versions(optimizer: torch.optim.Optimizer, args, kwargs) -> None:
+    """Optimizer step post-hook: mark every parameter of the optimizer as written in place."""
+    torch.autograd.graph.increment_version([p for g in optimizer.param_groups for p in g["params"]])
+
+
+def track_optimizer(optimizer: torch.optim.Optimizer):
+    """Keep `packed`'s weight caches honest under an optimizer that writes parameters without
+    bumping their version counter.  torch's fused Adam (fused=True) and the other fused/foreach
+    kernels update the storage in place through a raw kernel: p._version stays unchanged and the
+    data_ptr too, so a cached bf16 pack would outlive the update.  This installs a step post-hook
+    that bumps every parameter's version after each step(); returns the hook handle.  Brain does
+    this for its own optimizer; any other optimizer driving an MFMA Network must too."""
+    return optimizer.register_step_post_hook(_bump_versions)
+
+
 def packed(weight: torch.Tensor, kind: str, fn) -> torch.Tensor:
     """fn(weight) — a kernel-layout copy of a layer's weight — cached on the weight tensor until the
-    weight changes (its in-place version counter: optimizer steps and load_state_dict bump it).  One
-    training step runs the online network three times (acting, Q(s), Q(s')) and packs its weights
-    once; the target network's packs live until the next sync."""
+    weight changes (its in-place version counter: load_state_dict's copy_ and autograd-visible
+    in-place ops bump it; a fused optimizer does NOT — see track_optimizer).  One training step runs
+    the online network three times (acting, Q(s), Q(s')) and packs its weights once; the target
+    network's packs live until the next sync."""
     stamp = (weight._version, weight.data_ptr())
     cache = getattr(weight, "_ffmp_packs", None)
     if cache is None:

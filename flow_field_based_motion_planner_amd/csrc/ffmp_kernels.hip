@@ -1633,6 +1633,30 @@ int raster_format(bool compact, int grid, int32_t flags) {
   return grid % 16 == 0 ? FMT_CT16 : FMT_CT4;
 }
 
+// The scripted reactive controller of ffmp_policy_reactive: one thread per env reads the env's
+// relative goal and a short ray of cells ahead of the robot on its newest frame (row index = ego
+// x = heading, ffmp_device.h cell_coord), and picks the action id 7 * vi + wi (config.py:25-58).
+template <typename T>
+__global__ __launch_bounds__(256) void policy_reactive_kernel(int64_t n, int32_t grid, const T* __restrict__ newest,
+                                                              int64_t env_stride, const float* __restrict__ state_g,
+                                                              int32_t look0, int32_t look1, float slow_dist,
+                                                              int64_t* __restrict__ action) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const float2 g = reinterpret_cast<const float2*>(state_g)[e];
+  int wi = (int)rintf(g.y / 0.2f) + 3;  // turn towards the goal (orient > 0: to the left, w > 0)
+  wi = wi < 0 ? 0 : wi > 6 ? 6 : wi;
+  const T* f = newest + e * env_stride + (int64_t)(grid / 2) * grid + grid / 2;
+  bool blocked = false;
+  for (int d = look0; d <= look1; ++d) blocked |= f[(int64_t)d * grid] > (T)0;
+  int vi = g.x < slow_dist ? 1 : 3;
+  if (blocked) {
+    vi = 0;
+    if (wi == 3) wi = 6;  // obstacle straight ahead and the goal too: turn on the spot (left)
+  }
+  action[e] = 7 * vi + wi;
+}
+
 // Calls f(NT, XCD, FLOW, FMT) with std::integral_constant arguments for the runtime choice (the
 // compact formats' flow planes are binary16).
 template <class F>
@@ -1940,9 +1964,10 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
 #endif
 static constexpr double kSkewEnvSpan = FFMP_SKEW_ENV_SPAN;
 
-int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
-                     ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
-                     int32_t cells_per_block, int32_t flags, void* stream) {
+// ffmp_step_skewed; dry_run: every check (the LDS fit included), no launch (ffmp_step_skewed_check)
+static int step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
+                       ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
+                       int32_t cells_per_block, int32_t flags, void* stream, bool dry_run) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
   if (n < 0 || env_offset < 0) return fail(FFMP_E_ARG, "negative n or env_offset");
@@ -2008,6 +2033,7 @@ int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const
                  : (size_t)0;
     }();
     if (static_lds + keys > device_lds_limit()) return false;
+    if (dry_run) return true;
     hipLaunchKernelGGL((skew_kernel<kNT, kXCD, kL>), grid, block, keys, s, *cfg, n, env_offset, action_next, *state_next,
                        *obs, o, (int32_t)env_chunks, (int32_t)chunk_s, bpe, cpb, record_raster, sm_stride, sm_frame,
                        newest, tile_log2r);
@@ -2025,7 +2051,33 @@ int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const
   };
   const bool ok = nt ? (xcd ? with_l(T{}, T{}) : with_l(T{}, N{})) : (xcd ? with_l(N{}, T{}) : with_l(N{}, N{}));
   if (!ok) return fail(FFMP_E_ARG, "ffmp_step_skewed: the env waves' LDS does not fit (L = %d)", cfg->n_beams);
+  if (dry_run) return FFMP_OK;
   return check_launch("ffmp_step_skewed");
+}
+
+int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
+                     ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
+                     int32_t cells_per_block, int32_t flags, void* stream) {
+  return step_skewed(cfg, n, env_offset, action_next, state_next, obs, out, record_raster, cells_per_block, flags,
+                     stream, false);
+}
+
+int ffmp_step_skewed_check(const ffmp_cfg_t* cfg, int32_t format, int32_t flags) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (format != FFMP_OBS_F32 || cfg->flow) return fail(FFMP_E_ARG, "ffmp_step_skewed: float32 frames without flow planes only");
+  if (cfg->n_obst > FFMP_MAX_OBST) return fail(FFMP_E_ARG, "n_obst > FFMP_MAX_OBST");
+  // the launch's own checks on a placeholder batch of one env, stopped before the launch
+  static double dummy[8];
+  static float fdummy[64];
+  static int32_t idummy[2];
+  static uint32_t udummy[1];
+  static uint8_t bdummy[4];
+  static int64_t adummy[1];
+  ffmp_state_t st{dummy, dummy, dummy, dummy, dummy, idummy, idummy, fdummy, udummy, nullptr, nullptr};
+  ffmp_obs_t ob{fdummy, fdummy, fdummy, fdummy, nullptr, fdummy, fdummy, nullptr, 0, 0, FFMP_OBS_F32, 0};
+  ffmp_out_t o{fdummy, bdummy, bdummy + 1, bdummy + 2, bdummy + 3};
+  return step_skewed(cfg, 1, 0, adummy, &st, &ob, &o, fdummy + 32, 0, flags & ~FFMP_RASTER_NEWEST, nullptr, true);
 }
 
 int ffmp_reward_done(const ffmp_cfg_t* cfg, int64_t n, const double* scan, int32_t scan_len,
@@ -2212,6 +2264,31 @@ int ffmp_bev_image(int64_t n, int32_t compact, const void* occ, int64_t occ_env_
     hipLaunchKernelGGL((bev_image_kernel<false, 1>), grid, dim3(256), 0, s, n, occ, occ_env_stride, flow, plane,
                        (int32_t)chunks, vmax, out, out_env_stride);
   return check_launch("ffmp_bev_image");
+}
+
+int ffmp_policy_reactive(const ffmp_cfg_t* cfg, int64_t n, const ffmp_obs_t* obs, int64_t* action, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n < 0) return fail(FFMP_E_ARG, "negative n");
+  if (!obs || !obs->state_m || !obs->state_g || !action) return fail(FFMP_E_ARG, "obs.state_m / obs.state_g / action is NULL");
+  if (obs->format != FFMP_OBS_F32 && obs->format != FFMP_OBS_U8F16) return fail(FFMP_E_ARG, "unknown obs format %d", obs->format);
+  if (n == 0) return FFMP_OK;
+  const int64_t G2 = (int64_t)cfg->grid * cfg->grid;
+  const int64_t env_stride = obs->state_m_stride ? obs->state_m_stride : 2 * G2;
+  const int64_t frame = obs->state_m_frame_stride ? obs->state_m_frame_stride : G2;
+  // the look-ahead ray: from just outside the footprint (3 cells) to ~0.4 m ahead, inside the map
+  const int32_t look0 = 3, look1 = std::min<int32_t>(3 + (int32_t)std::lround(0.25 / cfg->res), cfg->grid / 2 - 1);
+  if (look1 < look0) return fail(FFMP_E_ARG, "grid %d too small for the look-ahead", cfg->grid);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (obs->format == FFMP_OBS_F32)
+    hipLaunchKernelGGL(policy_reactive_kernel<float>, grid, block, 0, s, n, cfg->grid, obs->state_m + frame, env_stride,
+                       obs->state_g, look0, look1, 1.0f, action);
+  else
+    hipLaunchKernelGGL(policy_reactive_kernel<uint8_t>, grid, block, 0, s, n, cfg->grid,
+                       reinterpret_cast<const uint8_t*>(obs->state_m) + frame, env_stride, obs->state_g, look0, look1,
+                       1.0f, action);
+  return check_launch("ffmp_policy_reactive");
 }
 
 #ifdef FFMP_TRACE

@@ -3,12 +3,12 @@
 Everything stays in HBM: transitions go into the device ReplayMemory (records), minibatches
 are re-rastered there, and the Q-networks run on the batch without host round trips.
 
-  Brain.__init__ (:307-314)                     -> same hyper-parameters (train.py:57-79)
-  Brain.decide_action (:337-349)                -> decide_action(obs, episode): per-env
+  Brain.__init__ (:307-314)                     -> same hyper-parameters (train.py:59-79)
+  Brain.decide_action (:336-347)                -> decide_action(obs, episode): per-env
       epsilon = 0.5 * (1 / (episode + 1)); greedy iff epsilon <= U(0,1); batched, per_sample
       coupling (= the reference's B = 1 forward for every env)
-  Brain.replay (:316-334) + make_minibatch (:352-372)
-      + get_expected_state_action_values (:374-412) + update_main_q_network (:414-428)
+  Brain.replay (:316-333) + make_minibatch (:349-369)
+      + get_expected_state_action_values (:371-411) + update_main_q_network (:413-428)
                                                 -> replay(): sample, Q(s,a), a* = argmax_a
       Q_main(s',a), y = r + GAMMA * Q_target(s', a*) (no terminal mask, as the reference;
       mask_terminal=True multiplies by 1 - done), MSE, Adam step
@@ -37,15 +37,16 @@ from typing import Dict, Optional
 import torch
 import torch.nn as nn
 
+from .conv_mfma import track_optimizer
 from .network import Network, map_channels
 from .replay import ReplayMemory
 
-GAMMA = 0.95            # train.py:57
-BATCH_SIZE = 1024       # train.py:62
-CAPACITY = 20000        # train.py:64
-LEARNING_RATE = 0.0005  # train.py:70
-NUM_ACTIONS = 28        # train.py:69
-INPUT_CHANNELS = 2      # train.py:68
+GAMMA = 0.95            # train.py:59
+BATCH_SIZE = 1024       # train.py:63
+CAPACITY = 20000        # train.py:65
+LEARNING_RATE = 0.0005  # train.py:71
+NUM_ACTIONS = 28        # train.py:70
+INPUT_CHANNELS = 2      # train.py:69
 
 
 class Brain:
@@ -96,6 +97,9 @@ class Brain:
         # ~0.15 ms per update at the reference's Network), the same update up to fp32 rounding
         self.optimizer = torch.optim.Adam(self.main_q_network.parameters(), lr=lr,
                                           fused=self.device.type == "cuda")
+        # the fused step writes the weights without bumping their version counters: bump them after
+        # every step, or the MFMA convolutions' cached bf16 weight packs would go stale
+        track_optimizer(self.optimizer)
         self.loss: Optional[torch.Tensor] = None
         self.step = 0
         self.gen = torch.Generator(device=self.device)
@@ -116,7 +120,7 @@ class Brain:
             net.coupling = prev
 
     def decide_action(self, obs: Dict[str, torch.Tensor], episode: torch.Tensor) -> torch.Tensor:
-        """Epsilon-greedy actions (N,) int64 for every env (train.py:337-349).  With temporal_maps
+        """Epsilon-greedy actions (N,) int64 for every env (train.py:336-347).  With temporal_maps
         the map input is the env's k-frame series (FFMPVec.temporal_maps), not obs["state_m"]."""
         n = obs["state_m"].shape[0]
         if self.temporal_maps:

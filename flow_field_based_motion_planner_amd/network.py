@@ -67,7 +67,7 @@ class Network(nn.Module):
                 torch.get_autocast_dtype("cuda") == torch.bfloat16:
             if conv_mfma.supported(conv, x.shape):
                 return conv_mfma.conv_relu(conv, x)
-            if conv_mfma.fold_supported(conv, x.shape):  # conv1: 1 / 2 / 3 / 4 map channels
+            if conv_mfma.fold_supported(conv, x.shape):  # conv1: 1-16 map channels (padded to 2^k)
                 return conv_mfma.fold_conv_relu(conv, x)
         return F.relu(conv(x))
 

@@ -89,6 +89,9 @@ class FFMPVec:
             a ring `bev` (k, N, 4, G, G) written after every step / reset; bev_maps() is the input of
             the reference's 12-channel option (train.py:66: "(occupancy(MONO) + flow(RGB)) *
             series(3 steps)", k = 3).  One extra elementwise launch per step.
+        info_format: "dict" (default): step()'s info is one dict of (N,) device tensors (is_goal,
+            collision, truncated, step, episode).  "list": gym 0.17/0.18 VectorEnv's form, a tuple
+            of N per-env dicts of Python scalars (one device -> host copy per step).
     """
 
     def __init__(self, num_envs: int, config: Union[FFMPConfig, str] = "C3",
@@ -97,7 +100,7 @@ class FFMPVec:
                  autotune: bool = True, pipeline: Optional[int] = None, keep_terminal: bool = False,
                  frame_window: Optional[int] = None, seamless: Optional[bool] = None,
                  fused: Optional[bool] = None, tuning: Optional[dict] = None, obs_format: str = "f32",
-                 hbm_budget: Optional[int] = None, bev_series: int = 0):
+                 hbm_budget: Optional[int] = None, bev_series: int = 0, info_format: str = "dict"):
         if isinstance(config, str):
             config = preset(config)
         if seed is not None:
@@ -117,6 +120,9 @@ class FFMPVec:
         if obs_format not in self.OBS_FORMATS:
             raise ValueError(f"obs_format must be one of {sorted(self.OBS_FORMATS)}, got {obs_format!r}")
         self.obs_format = obs_format
+        if info_format not in self.INFO_FORMATS:
+            raise ValueError(f"info_format must be one of {self.INFO_FORMATS}, got {info_format!r}")
+        self.info_format = info_format
         self._fmt, self._frame_dtype, self._pot_dtype = self.OBS_FORMATS[obs_format]
         self._fes = torch.empty((), dtype=self._frame_dtype).element_size()  # bytes per frame cell
         self._pes = torch.empty((), dtype=self._pot_dtype).element_size()    # bytes per potential cell
@@ -1143,8 +1149,7 @@ class FFMPVec:
         self._check_open()
         with torch.cuda.device(self.device):
             if seed is not None:
-                self.cfg = self.cfg.replace(seed=int(seed))
-                self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
+                self._set_cfg(self.cfg.replace(seed=int(seed)))
             m = None
             if mask is not None:
                 m = mask.to(device=self.device, dtype=torch.bool).contiguous().view(torch.uint8)
@@ -1272,12 +1277,15 @@ class FFMPVec:
         """Advance every env one step. Returns (obs, reward f32[N], done bool[N], info).
 
         `timing`: optional list; (start, end, n_envs, algorithmic bytes, full) per raster launch
-        (HIP events on the caller's stream) are appended to it."""
+        (HIP events on the caller's stream) are appended to it.  With use_graphs(True) (and no
+        `timing`) the step's launches run as the replay of a single-step HIP graph (step_graphs)."""
         self._check_open()
         if self._needs_reset:
             raise RuntimeError("call reset() before step()")
         with torch.cuda.device(self.device):
-            if self.pipeline_slices > 1:
+            if self._graphs is not None and timing is None:
+                self._step_graph(actions)
+            elif self.pipeline_slices > 1:
                 self._step_pipelined(actions, timing)
             elif self.fused:
                 self._step_fused(actions, timing)
@@ -1285,12 +1293,100 @@ class FFMPVec:
                 self.step_state(actions)
                 self.raster_step(timing)
             self._bev_push(advance=True)
-        info = {"is_goal": self.is_goal, "collision": self.collision, "truncated": self.truncated,
-                "step": self.t, "episode": self.episode}
+        if self.info_format == "list":
+            info = self._info_list()
+        else:
+            info = {"is_goal": self.is_goal, "collision": self.collision, "truncated": self.truncated,
+                    "step": self.t, "episode": self.episode}
+            if copy:
+                info = {k: v.clone() for k, v in info.items()}
         if copy:
-            info = {k: v.clone() for k, v in info.items()}
             return self._obs_out(True), self.reward.clone(), self.done.clone(), info
         return self.obs, self.reward, self.done, info
+
+    # ------------------------------------------------ info in gym 0.17/0.18's per-env form
+    # "dict" (default): one dict of (N,) device tensors, the batched form (nothing leaves the GPU).
+    # "list": gym.vector.VectorEnv.step_wait's form in gym 0.17/0.18 — a tuple of N dicts of Python
+    # scalars, one per env (costs one device -> host copy of the five (N,) flags per step).
+    info_format = "dict"
+    INFO_FORMATS = ("dict", "list")
+
+    def _info_list(self) -> tuple:
+        keys = ("is_goal", "collision", "truncated", "step", "episode")
+        cols = torch.stack([getattr(self, k).to(torch.int64) for k in keys]).cpu().tolist()
+        return tuple({"is_goal": bool(g), "collision": bool(c), "truncated": bool(tr), "step": int(st),
+                      "episode": int(ep)} for g, c, tr, st, ep in zip(*cols))
+
+    # ------------------------------------------------ single-step graphs for step()
+    # A closed-loop caller (each action computed from the previous observation, train.py:572-577)
+    # cannot use capture()'s multi-step graphs.  use_graphs(True): every step() replays a HIP graph of
+    # ONE step (its env kernel + raster, or the one-launch step), captured lazily for each frame-ring
+    # position (graph_period() of them), reading the actions from a static device buffer
+    # (`action_buffer`; step(env.action_buffer) skips the copy into it).  Bit-identical to the plain
+    # launches (tests/test_gpu_graph.py).
+    _graphs = None
+
+    def use_graphs(self, on: bool = True) -> None:
+        """Run step() as single-step graph replays (on) or plain launches (off).  Not with pipeline
+        slices or a BEV image ring (their steps need per-step host work)."""
+        self._check_open()
+        if not on:
+            self._graphs = None
+            return
+        if self.pipeline_slices > 1 or self.bev is not None:
+            raise ValueError("use_graphs() needs pipeline=1 and no bev_series")
+        if self._graphs is None:
+            self._graphs = {}
+            if getattr(self, "action_buffer", None) is None:
+                self.action_buffer = torch.zeros(self.num_envs, dtype=torch.int64, device=self.device)
+
+    action_buffer = None
+
+    def _step_graph(self, actions) -> None:
+        buf = self.action_buffer
+        if not (isinstance(actions, torch.Tensor) and actions.data_ptr() == buf.data_ptr()):
+            buf.copy_(self._actions(actions), non_blocking=True)
+        key = (self._wpos, self.fused)
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            snap = (self._wpos, list(self._hist), self._hist_from_reset)
+            stream = torch.cuda.Stream(device=self.device)
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            try:
+                with torch.cuda.graph(g, stream=stream):
+                    if self.fused:
+                        self._step_fused(buf)
+                    else:
+                        self.step_state(buf)
+                        self.raster_step()
+            finally:
+                # nothing ran: the host bookkeeping goes back to where the GPU state is
+                self._set_window(snap[0])
+                self._hist, self._hist_from_reset = snap[1], snap[2]
+            self._graphs[key] = g
+        g.replay()
+        self._next_window()
+
+    # ------------------------------------------------ closed-loop controller
+    def policy_reactive(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The next actions (N,) int64 from the current observation, on the device
+        (include/ffmp.h ffmp_policy_reactive: steer towards the goal, stop and turn when the newest
+        frame is occupied just ahead) — a scripted controller for closed-loop runs (bench.py's
+        closed_loop leg), not the reference's Q-network.  `out`: write into this (N,) int64 tensor
+        (e.g. action_buffer) instead of a new one."""
+        self._check_open()
+        if self._needs_reset:
+            raise RuntimeError("call reset() before policy_reactive()")
+        if out is None:
+            out = torch.empty(self.num_envs, dtype=torch.int64, device=self.device)
+        elif out.shape != (self.num_envs,) or out.dtype != torch.int64 or not out.is_contiguous() \
+                or out.device != self.device:
+            raise ValueError(f"out must be a contiguous int64 tensor of shape ({self.num_envs},) on {self.device}")
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.ffmp_policy_reactive(C.byref(self._cfg_c), self.num_envs, C.byref(self._obs_c),
+                                                     out.data_ptr(), self._stream()), "ffmp_policy_reactive")
+        return out
 
     # ------------------------------------------------ HIP graph of whole steps
     def graph_period(self) -> int:
@@ -1302,7 +1398,7 @@ class FFMPVec:
         return self.frame_window - 1 if self.frame_window > 2 else 1
 
     def capture(self, steps: Optional[int] = None, pipelined: Optional[bool] = None,
-                skewed: Optional[bool] = None) -> "StepGraph":
+                skewed: Optional[bool] = None, policy=None) -> "StepGraph":
         """Capture `steps` consecutive steps (default graph_period(); a multiple of it) into one HIP
         graph (torch.cuda.CUDAGraph: hipGraph on ROCm).  StepGraph.replay(actions) then runs them as
         ONE launch from the host — every kernel of every step, the same launches step() makes, with
@@ -1312,8 +1408,13 @@ class FFMPVec:
         default, StepGraph.PIPELINE_DEFAULT): the env kernel of step i + 1 runs beside the raster of
         step i (see StepGraph).  `skewed` (float32 frames, no flow planes, the two-launch step, an even
         count; by default where the env step's blocks fit the CUs once, StepGraph._skew_pays): the
-        raster of step i and the env step of step i + 1 in ONE launch (ffmp_step_skewed)."""
-        return StepGraph(self, steps, pipelined, skewed)
+        raster of step i and the env step of step i + 1 in ONE launch (ffmp_step_skewed).
+        `policy` (closed loop): "reactive" (policy_reactive) or a callable env -> (N,) int64 device
+        tensor, captured too: each step's actions are computed inside the graph from the previous
+        step's observation (the first from the observation before the replay), and replay() takes
+        no actions — the device-resident form of train.py:572-577's act-then-publish loop.  Plain
+        two-launch (or one-launch) steps only: the policy reads the raster's frame."""
+        return StepGraph(self, steps, pipelined, skewed, policy)
 
     # ------------------------------------------------ gym.vector.VectorEnv surface
     is_vector_env = True
@@ -1365,8 +1466,15 @@ class FFMPVec:
 
     def seed(self, seed: int) -> None:
         """gym 0.17-style: the seed of the next full reset()."""
-        self.cfg = self.cfg.replace(seed=int(seed))
+        self._set_cfg(self.cfg.replace(seed=int(seed)))
+
+    def _set_cfg(self, cfg: FFMPConfig) -> None:
+        """A new config after construction (a new seed): the launch struct is rebuilt, and the
+        single-step graphs, which captured the old one by value, are dropped (re-captured on use)."""
+        self.cfg = cfg
         self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
+        if self._graphs is not None:
+            self._graphs = {}
 
     def step_async(self, actions) -> None:
         self._pending_actions = actions
@@ -1385,6 +1493,8 @@ class FFMPVec:
         self._closed = True
         self._needs_reset = True
         torch.cuda.synchronize(self.device)
+        self._graphs = None  # their kernels' arguments point into the buffers freed below
+        self.action_buffer = None
         for name, _, _ in self._buffer_specs():
             setattr(self, name, None)
         # the launch structs hold raw device pointers into the freed buffers
@@ -1447,8 +1557,7 @@ class FFMPVec:
                 v.copy_(sd[k])
         seed = int(sd["seed"])
         if seed != self.cfg.seed:
-            self.cfg = self.cfg.replace(seed=seed)
-            self._cfg_c = _abi.make_cfg(self.cfg, _ptr(self.beam_cs) or 0)
+            self._set_cfg(self.cfg.replace(seed=seed))
         self.raster()
         self._hist, self._hist_from_reset = [], False  # older frames than the pair are not restored
         self._note_window(True)
@@ -1515,13 +1624,13 @@ class StepGraph:
 
     @staticmethod
     def skew_supported(env: FFMPVec, k: int) -> bool:
-        """Does ffmp_step_skewed take this instance's steps (include/ffmp.h: float32 frames, no flow
-        planes; its env waves' LDS: 22.5 KiB of disc arrays + 4 x envs-per-wave x L beam words)?"""
+        """Does ffmp_step_skewed take this instance's steps?  The library answers
+        (ffmp_step_skewed_check: float32 frames, no flow planes, its env waves' LDS against the
+        device's limit) for both raster shapes the graph uses; the two-launch step and an even k."""
         if env.fused or k % 2 or env.obs_format != "f32" or env.flow is not None:
             return False
-        K = env.cfg.n_obst
-        lpe = 8 if K <= 8 else 16 if K <= 16 else 32 if K <= 32 else 64
-        return 22560 + 4 * (64 // lpe) * env.cfg.n_beams * 4 <= 64 * 1024
+        return all(env.lib.ffmp_step_skewed_check(C.byref(env._cfg_c), env._fmt, flags) == 0
+                   for flags in {env.raster_shape[1], env.raster_shape_newest[1]})
 
     @staticmethod
     def _skew_pays(env: FFMPVec) -> bool:
@@ -1534,8 +1643,15 @@ class StepGraph:
         return blocks <= torch.cuda.get_device_properties(env.device).multi_processor_count
 
     def __init__(self, env: FFMPVec, steps: Optional[int] = None, pipelined: Optional[bool] = None,
-                 skewed: Optional[bool] = None):
+                 skewed: Optional[bool] = None, policy=None):
         env._check_open()
+        if policy is not None:
+            if pipelined or skewed:
+                raise ValueError("a closed-loop graph (policy) runs plain steps: the policy reads each raster's frame")
+            if policy != "reactive" and not callable(policy):
+                raise ValueError("policy must be 'reactive' or a callable env -> (N,) int64 tensor")
+            pipelined = skewed = False
+        self.policy = policy
         if env._needs_reset:
             raise RuntimeError("call reset() before capture()")
         if env.pipeline_slices > 1 or env.bev is not None:
@@ -1582,6 +1698,8 @@ class StepGraph:
                     self._capture_skewed(k, bufs)
                 else:
                     for i in range(k):
+                        if policy is not None:
+                            self._act(i)
                         if env.fused:
                             env._step_fused(self.actions[i])
                         else:
@@ -1595,6 +1713,16 @@ class StepGraph:
             env._hist, env._hist_from_reset = snap[1], snap[2]
         if env._wpos != self.wpos:
             raise RuntimeError("frame position changed during capture")
+
+    def _act(self, i: int) -> None:
+        """Closed loop: step i's actions from the current observation, into the static block."""
+        if self.policy == "reactive":
+            self.env.policy_reactive(out=self.actions[i])
+        else:
+            a = self.policy(self.env)
+            if not (isinstance(a, torch.Tensor) and a.numel() == self.env.num_envs):
+                raise ValueError("policy must return an (N,) tensor of action ids")
+            self.actions[i].copy_(a.reshape(-1))
 
     def _capture_pipelined(self, k: int, bufs) -> None:
         env, side = self.env, self._side
@@ -1649,6 +1777,8 @@ class StepGraph:
         if env._wpos != self.wpos:
             raise RuntimeError("the env's frame position moved since capture (step() a whole graph_period())")
         if actions is not None:
+            if self.policy is not None:
+                raise ValueError("a closed-loop graph computes its own actions (replay() takes none)")
             a = torch.as_tensor(actions)
             if a.shape != self.actions.shape:
                 raise ValueError(f"actions must have shape {tuple(self.actions.shape)}")

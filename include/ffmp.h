@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 7
+#define FFMP_ABI_VERSION 8  /* 8: ffmp_step_skewed_check, ffmp_policy_reactive */
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -267,6 +267,25 @@ int ffmp_step_fused(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const 
 int ffmp_step_skewed(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset, const int64_t* action_next,
                      ffmp_state_t* state_next, ffmp_obs_t* obs, ffmp_out_t* out, const float* record_raster,
                      int32_t cells_per_block, int32_t flags, void* stream);
+/* Would ffmp_step_skewed take steps of this config in this obs format with these raster flags
+ * (FFMP_RASTER_NT / PLAIN / XCD; NEWEST ignored)?  Runs every check of the launch — the env waves'
+ * LDS (static arrays + 4 x envs-per-wave x L beam words) against the device's limit included — and
+ * launches nothing.  FFMP_OK, or FFMP_E_ARG with the reason in ffmp_last_error().  A caller that
+ * captures skewed step graphs asks this first (FFMPVec.capture) instead of re-deriving the LDS need. */
+int ffmp_step_skewed_check(const ffmp_cfg_t* cfg, int32_t format, int32_t flags);
+
+/* A scripted reactive controller — no reference counterpart (the reference's actions come from its
+ * Q-network, src/train.py:336-347, published as /cmd_vel :665-682) — for closed-loop runs in which
+ * step t + 1's action must be computed on the device from step t's observation (benchmarks, demos,
+ * smoke tests).  Per env, from obs (the layout ffmp_step / ffmp_raster wrote: state_m's newest frame
+ * through its strides and format, state_g):
+ *   wi = clamp(rint(orient / 0.2) + 3, 0, 6)               (steer towards the goal)
+ *   blocked = any newest-frame cell on the heading ray, rows G/2 + 3 .. G/2 + 3 + round(0.25 / res)
+ *             of column G/2, is occupied (> 0)
+ *   vi = blocked ? 0 : (dist < 1.0 m ? 1 : 3); blocked with wi == 3 -> wi = 6 (turn in place)
+ *   action[e] = 7 * vi + wi   (RobotAction.cmd order, src/gym_ffmp/envs/robot/config.py:25-58)
+ * action: (n) int64 device memory.  One thread per env, reads 8 + (look-ahead) cells' bytes. */
+int ffmp_policy_reactive(const ffmp_cfg_t* cfg, int64_t n, const ffmp_obs_t* obs, int64_t* action, void* stream);
 
 /* ffmp_step_state + ffmp_raster. */
 int ffmp_step(const ffmp_cfg_t* cfg, int64_t n, int64_t env_offset,
@@ -469,7 +488,11 @@ int ffmp_bev_image(int64_t n, int32_t compact, const void* occ, int64_t occ_env_
  *   store probe, which overwrites the partner's bytes) to pair well with the partner bytes the
  *   raster writes beside it: the same offset when partner_bytes < 1.5 x slot_bytes (float32
  *   frames beside a float32 plane), twice the offset otherwise (uint8 frames beside a binary16
- *   plane, FFMP_OBS_U8F16).  NULL: no pairing.
+ *   plane, FFMP_OBS_U8F16).  NULL: no pairing.  The library remembers the best probe per partner
+ *   ADDRESS (the pairing reference, see ffmp_ring_pair_forget): a caller that passes a partner
+ *   MUST call ffmp_ring_pair_forget(device, partner) when it frees that plane, or a plane
+ *   allocated later at the same address inherits the old plane's reference (ffmp_ring_pool_trim
+ *   does not forget them since ABI 8).
  *   *base = the first virtual slot (device pointer); contents undefined.
  * Returns 0, FFMP_E_ARG, or FFMP_E_HIP (no VMM support, out of memory, ...; then use a plain
  * ring — ffmp_last_error() says which call failed).

@@ -26,6 +26,33 @@ def test_pack_cache_reuses_until_the_weight_changes():
     assert a3 is not a2 and int(a3.float().abs().sum()) == 0
 
 
+def test_fused_optimizer_step_invalidates_packs():
+    """torch's fused Adam writes parameters without bumping _version (ADVICE r05): track_optimizer's
+    step post-hook must bump it, or the cached packs would outlive every update."""
+    conv = torch.nn.Conv2d(32, 64, kernel_size=4)
+    w = conv.weight
+    opt = torch.optim.Adam(conv.parameters(), lr=0.1, fused=True)
+    conv(torch.randn(2, 32, 8, 8)).sum().backward()
+    v0 = w._version
+    opt.step()
+    assert w._version == v0  # the hazard itself: the fused step leaves the version alone
+    a = conv_mfma.packed(w, "fwd", conv_mfma.pack_weight)
+    conv_mfma.track_optimizer(opt)
+    for _ in range(2):
+        conv(torch.randn(2, 32, 8, 8)).sum().backward()
+        opt.step()
+        a2 = conv_mfma.packed(w, "fwd", conv_mfma.pack_weight)
+        assert a2 is not a and torch.equal(a2, conv_mfma.pack_weight(w)) and not torch.equal(a2, a)
+        a = a2
+
+
+def test_brain_tracks_its_optimizer():
+    """Brain's Adam carries the version-bumping hook (learner.py)."""
+    from flow_field_based_motion_planner_amd.learner import Brain
+    import inspect
+    assert "track_optimizer(self.optimizer)" in inspect.getsource(Brain.__init__)
+
+
 def test_pack_cache_without_attributes_falls_back():
     class NoAttr(torch.Tensor):
         def __setattr__(self, name, value):

@@ -211,3 +211,31 @@ def test_amp_at_a_grid_outside_the_kernels_falls_back_per_layer():
     sides = sorted({s[2] for s in calls})
     assert {65, 34, 27, 20} <= set(sides) and 13 not in sides, sides  # conv2, conv3, conv4 x2 on MFMA
     assert not conv_mfma.supported(b16.main_q_network.conv4, (32, 64, 13, 13))
+
+
+def test_amp_mfma_forward_tracks_fused_adam_updates():
+    """fused Adam writes the weights without bumping _version, so the MFMA
+    convolutions' cached bf16 packs went stale after the first update.  After two replay() updates
+    under amp + mfma, the next MFMA conv forward must equal F.conv2d on the CURRENT weights (bf16
+    autocast) — not on the initial ones."""
+    import torch.nn.functional as F
+    from flow_field_based_motion_planner_amd import conv_mfma
+    env = _env()
+    brain = Brain(env, capacity=256, batch_size=48, seed=7, amp=True, lr=5e-3)
+    _fill(brain, env, 3)
+    net = brain.main_q_network
+    w0 = net.conv2.weight.detach().clone()
+    x = torch.rand(4, 32, 69, 69, device=DEV)
+    for _ in range(2):
+        brain.replay(index=torch.randperm(len(brain.memory), device=DEV)[:48])
+    torch.cuda.synchronize()
+    assert not torch.equal(net.conv2.weight, w0)
+    with torch.no_grad(), torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        got = conv_mfma.conv_relu(net.conv2, x).float()
+        ref = F.relu(F.conv2d(x, net.conv2.weight, net.conv2.bias)).float()
+        stale = F.relu(F.conv2d(x, w0, net.conv2.bias)).float()
+    scale = float(ref.abs().max()) + 1e-6
+    err = float((got - ref).abs().max()) / scale
+    err_stale = float((got - stale).abs().max()) / scale
+    assert err < 2e-2, (err, err_stale)
+    assert err < err_stale

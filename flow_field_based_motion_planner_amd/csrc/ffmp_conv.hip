@@ -34,6 +34,14 @@ namespace ffmp_detail {
 int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_error())
 // ffmp_conv2d_check: run every shape check of a launch, then return before launching
 thread_local bool t_conv_dry = false;
+// the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 16 = 16x16x32
+// (default), 32 = 32x32x16
+int g_conv_mfma = 16;
+int conv_mfma_swap(int v) {
+  const int prev = g_conv_mfma;
+  g_conv_mfma = v;
+  return prev;
+}
 }
 using ffmp_detail::fail;
 using ffmp_detail::t_conv_dry;
@@ -138,19 +146,51 @@ __device__ __forceinline__ bf16x8 load_bfrag(const __bf16* __restrict__ w, int t
 #ifndef FFMP_CONV_FWD_OCC
 #define FFMP_CONV_FWD_OCC 2  // workgroups per CU the forward kernel is compiled for
 #endif
-template <int C, int NB, int MBW, bool PAD, bool WF>
+// MFMA shape MS: 32 = v_mfma_f32_32x32x16_bf16 (32-position x 32-channel blocks, k-steps of 16
+// channels), 16 = v_mfma_f32_16x16x32_bf16 (16 x 16 blocks, k-steps of 32) at the same output tile
+// per wave — the same FLOPs, A/B bytes and accumulator registers, but the chip holds a higher clock
+// on the 16x16x32 stream (MI355X_MICROARCH.md, DVFS give-back item 7: ~1.12-1.15x the FLOP/s on
+// random data).  Lane l of a 16x16x32 operand holds row l & 15, k = 8 (l >> 4) .. +8; its C/D
+// element i is row 4 (l >> 4) + i, column l & 15.
+template <int MS>
+struct Mfma;
+template <>
+struct Mfma<32> {
+  typedef f32x16 acc_t;
+  static constexpr int KS = 16, NACC = 16;
+  static __device__ __forceinline__ acc_t mma(bf16x8 a, bf16x8 b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int row(int i, int kh) { return (i & 3) + 8 * (i >> 2) + 4 * kh; }
+};
+template <>
+struct Mfma<16> {
+  typedef f32x4 acc_t;
+  static constexpr int KS = 32, NACC = 4;
+  static __device__ __forceinline__ acc_t mma(bf16x8 a, bf16x8 b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int row(int i, int kh) { return 4 * kh + i; }
+};
+
+
+template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  using M = Mfma<MS>;
   constexpr int N = NB * 32;
   constexpr int PT = kWaves * MBW * 32;
+  constexpr int AM = MBW * 32 / MS, AN = N / MS;  // MFMA blocks per wave: positions x channels
+  constexpr int KSTEPS = C / M::KS;                // k-steps per tap
+  static_assert(!WF || MS == 32, "fragment-order weights are laid out for the 32x32x16 operand");
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const int b = blockIdx.y;
   const int P = Ho * Wo;
   const int p0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
+  const int r = lane & (MS - 1), kh = lane / MS;  // operand row, k-chunk of 8 channels
   const int rowbytes = W * C * 2;      // one tensor row (of the folded image with FFMP_CONV_X_FOLD)
   const int pitch = lds_pitch<C>(W);   // its padded image = one ring slot
   const int chunks = rowbytes / 16;    // <= 4 * 256 (host check)
@@ -168,10 +208,10 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
 
   // this lane's output positions (clamped into the image; out-of-range ones are not stored):
   // output row, and input column of kernel column 0 relative to the tensor (xp - pad)
-  int ypos[MBW], xcol[MBW];
+  int ypos[AM], xcol[AM];
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb) {
-    const int m = min(p0 + (wave * MBW + mb) * 32 + r, P - 1);
+  for (int mb = 0; mb < AM; ++mb) {
+    const int m = min(pw0 + mb * MS + r, P - 1);
     ypos[mb] = m / Wo;
     xcol[mb] = m - ypos[mb] * Wo - pad;
   }
@@ -188,27 +228,31 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
 
-  f32x16 acc[MBW][NB];
+  typename M::acc_t acc[AM][AN];
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
+  for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x16{};
+    for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = typename M::acc_t{};
 
   // B fragments of the wave's first tap (wk_lo, 0); from then on loaded one tap ahead (the active
   // kernel rows [wk_lo, wk_hi] are consecutive, so the tap after t is t + 1, up to the wave's last
   // tap, which later loads re-read)
   const int t_last = min(wk_hi, KH - 1) * KW + KW - 1;
-  auto load_b = [&](int t, bf16x8 (&dst)[NB][C / 16]) {
+  auto load_b = [&](int t, bf16x8 (&dst)[AN][KSTEPS]) {
     t = min(t, t_last);
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-      for (int s = 0; s < C / 16; ++s)
-        dst[nb][s] = load_bfrag<C, NB, WF>(w, t, nb, s, r, h);
+      for (int s = 0; s < KSTEPS; ++s) {
+        if constexpr (MS == 32)
+          dst[nb][s] = load_bfrag<C, NB, WF>(w, t, nb, s, r, kh);
+        else  // w [KH][KW][N][C]: row n = nb * 16 + r, channels s * 32 + 8 kh .. +8
+          dst[nb][s] = *(const bf16x8*)(w + ((size_t)(t * N + nb * 16 + r) * C + s * 32 + kh * 8));
+      }
   };
   constexpr int kBAhead = FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
-  bf16x8 bcur[NB][C / 16];
-  bf16x8 bnx[NB][C / 16];  // kBAhead 2: the ping-pong partner of bcur
+  bf16x8 bcur[AN][KSTEPS];
+  bf16x8 bnx[AN][KSTEPS];  // kBAhead 2: the ping-pong partner of bcur
   load_b(min(wk_lo, KH - 1) * KW, bcur);
 
   for (int ky = ky_lo; ky <= ky_hi; ++ky) {
@@ -216,28 +260,27 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
     const bool more = ky < ky_hi;
     if (more) load_row_regs<C>(row_src(yl + ky + 1), chunks, gin.x, nrow);
     if (ky >= wk_lo && ky <= wk_hi) {
-      int aoff[MBW];
+      int aoff[AM];
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
+      for (int mb = 0; mb < AM; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
       // the MFMAs of tap (ky, kx) with its B fragments
-      auto tap = [&](int kx, const bf16x8 (&bt)[NB][C / 16]) {
+      auto tap = [&](int kx, const bf16x8 (&bt)[AN][KSTEPS]) {
         // the lane's column of each block, or the zero column outside the tensor (PAD)
-        int abase[MBW];
+        int abase[AM];
 #pragma unroll
-        for (int mb = 0; mb < MBW; ++mb) {
+        for (int mb = 0; mb < AM; ++mb) {
           const int col = xcol[mb] + kx * dx;
-          abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + h * 16;
+          abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + kh * 16;
         }
 #pragma unroll
-        for (int s = 0; s < C / 16; ++s) {
-          bf16x8 a[MBW];
+        for (int s = 0; s < KSTEPS; ++s) {
+          bf16x8 a[AM];
 #pragma unroll
-          for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * 32);
+          for (int mb = 0; mb < AM; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
 #pragma unroll
-          for (int mb = 0; mb < MBW; ++mb)
+          for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bt[nb][s], acc[mb][nb], 0, 0, 0);
+            for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[mb], bt[nb][s], acc[mb][nb]);
         }
       };
       if constexpr (kBAhead == 2) {
@@ -254,19 +297,19 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
           load_b(ky * KW + kx + 1, bnx);
           tap(kx, bcur);
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
+          for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-            for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnx[nb][s];
+            for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnx[nb][s];
         }
       } else {
         for (int kx = 0; kx < KW; ++kx) {
-          bf16x8 bnext[NB][C / 16];
+          bf16x8 bnext[AN][KSTEPS];
           load_b(ky * KW + kx + 1, bnext);
           tap(kx, bcur);
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
+          for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-            for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
+            for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnext[nb][s];
         }
       }
     }
@@ -274,18 +317,18 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
     __syncthreads();
   }
 
-  // epilogue: C/D of 32x32x16: column = lane & 31 (channel), row = (i & 3) + 8 (i >> 2) + 4 h
+  // epilogue: C/D column = lane & (MS - 1) (channel), row = Mfma<MS>::row(i, kh) (position)
   const bool relu = flags & FFMP_CONV_RELU, out_bf16 = flags & FFMP_CONV_OUT_BF16;
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    const int n = nb * 32 + r;
+  for (int nb = 0; nb < AN; ++nb) {
+    const int n = nb * MS + r;
     const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb) {
-      const int mbase = p0 + (wave * MBW + mb) * 32;
+    for (int mb = 0; mb < AM; ++mb) {
+      const int mbase = pw0 + mb * MS;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = mbase + (i & 3) + 8 * (i >> 2) + 4 * h;
+      for (int i = 0; i < M::NACC; ++i) {
+        const int m = mbase + M::row(i, kh);
         if (m >= P) continue;
         float v = acc[mb][nb][i] + bn;
         if (relu) v = fmaxf(v, 0.f);
@@ -484,8 +527,12 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w, bias,
-                     y, H, W, KH, KW, pad, dx, ring, flags);
+  if (!WF && ffmp_detail::g_conv_mfma == 16)
+    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, false, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32>), grid, dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
   return FFMP_OK;

@@ -42,6 +42,7 @@ __attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
   return code;
 }
 int32_t ring_extra_swap(int32_t v);  // ffmp_ring.hip (FFMP_TUNE_RING_EXTRA)
+int conv_mfma_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_MFMA)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1721,6 +1722,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       prev = t.env_lanes;
       t.env_lanes = value;
       return prev;
+    case FFMP_TUNE_CONV_MFMA:
+      if (value != 16 && value != 32) return fail(FFMP_E_ARG, "conv MFMA shape must be 16 (16x16x32) or 32 (32x32x16)");
+      return ffmp_detail::conv_mfma_swap(value);
     case FFMP_TUNE_RING_EXTRA:
       if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");
       return ffmp_detail::ring_extra_swap(value);

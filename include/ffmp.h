@@ -179,7 +179,8 @@ const char* ffmp_last_error(void);
 int64_t ffmp_layout(int32_t which);
 
 /* Launch-shape tuning (process-wide; not thread-safe against concurrent launches).
- * Returns the previous value (>= 0) or FFMP_E_ARG.  Never changes results. */
+ * Returns the previous value (>= 0) or FFMP_E_ARG.  Never changes results (FFMP_TUNE_CONV_MFMA: the
+ * convolutions' fp32 summation order). */
 #define FFMP_TUNE_RASTER_CPB 1  /* raster cells per block: multiple of 1024; 0 = default   */
 #define FFMP_TUNE_RASTER_NT 2   /* raster stores: 0 by plane size, 1 plain, 2 nontemporal  */
 #define FFMP_TUNE_RASTER_XCD 3  /* 1: XCD-aware block remap                                */
@@ -189,6 +190,9 @@ int64_t ffmp_layout(int32_t which);
                                    ones the ring needs (pairing candidates; they stay pooled):
                                    0 = default (need/2 + 4), v >= 1 = at most v - 1.  An HBM
                                    budget (FFMPVec hbm_budget) sets it around its ring creation. */
+#define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 16 (default,
+                                   v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); the same
+                                   products, fp32 sums in another order */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

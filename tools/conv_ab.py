@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""A/B of the convolution kernels' MFMA shape (FFMP_TUNE_CONV_MFMA: 16 = 16x16x32, 32 = 32x32x16) on
+the reference Network's layers at batch B (default 256), random data, interleaved rounds in ONE process
+(cdna_hip_programming.md rule 24): per layer and shape the median / min ms and PF/s over the rounds,
+and each shape's max error against a float64 convolution of the same bf16 operands (first 4 samples).
+Usage: python tools/conv_ab.py [B] [rounds]"""
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flow_field_based_motion_planner_amd import _abi  # noqa: E402
+from flow_field_based_motion_planner_amd.conv_mfma import (conv2d_dgrad_nhwc, conv2d_nhwc, conv2d_wgrad_nhwc,  # noqa: E402
+                                                          fold_input, frag_order, nhwc_bf16, pack_weight,
+                                                          pack_weight_dgrad_bm, pack_weight_fold)
+
+dev = torch.device("cuda:0")
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+SHAPES = (16, 32)
+torch.manual_seed(0)
+
+
+def timeit(fn, reps=5):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+layers = {}
+# conv2: 32 -> 64, k 32, 69^2 -> 38^2 (forward, bias + ReLU, bf16 out)
+x2 = torch.relu(rnd(B, 69, 69, 32))
+w2 = rnd(64, 32, 32, 32, scale=1 / 181.0)
+b2 = torch.randn(64, device=dev)
+wp2 = pack_weight(w2)
+layers["conv2 fwd"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32,
+                       lambda: conv2d_nhwc(x2, wp2, b2, relu=True, out_dtype=torch.bfloat16),
+                       lambda: F.relu(F.conv2d(x2[:4].permute(0, 3, 1, 2).double(), w2.double(), b2.double())))
+# conv2's data gradient (samples as M) and weight gradient
+g2 = rnd(B, 38, 38, 64)
+wbm = pack_weight_dgrad_bm(w2)
+layers["conv2 dgrad_bm"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32, lambda: conv2d_dgrad_nhwc(g2, wbm),
+                            lambda: torch.ops.aten.convolution_backward(
+                                g2[:4].permute(0, 3, 1, 2).double(), x2[:4].permute(0, 3, 1, 2).double(), w2.double(),
+                                None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0])
+layers["conv2 wgrad"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32, lambda: conv2d_wgrad_nhwc(g2, x2, 32, 32), None)
+# conv1: 2 -> 32, k 32, 100^2 -> 69^2, folded (F = 16), bf16 out + ReLU
+x1 = torch.rand(B, 2, 100, 100, device=dev) * 255
+w1 = rnd(32, 2, 32, 32, scale=1 / 45.0)
+b1 = torch.randn(32, device=dev)
+wf1 = frag_order(pack_weight_fold(w1, 16))
+layers["conv1 fwd (fold)"] = (2.0 * B * 69 * 69 * 32 * 2 * 32 * 32,
+                              lambda: conv2d_nhwc(nhwc_bf16(x1), wf1, b1, relu=True, out_dtype=torch.bfloat16, dx=16,
+                                                  x_fold=True), None)
+# conv3: 64 -> 64, k 8, 38^2 -> 31^2 (small-image kernel, fragment-order weights)
+x3 = torch.relu(rnd(B, 38, 38, 64))
+w3 = rnd(64, 64, 8, 8, scale=1 / 22.6)
+b3 = torch.randn(64, device=dev)
+wf3 = frag_order(pack_weight(w3))
+layers["conv3 fwd (small)"] = (2.0 * B * 31 * 31 * 64 * 64 * 64, lambda: conv2d_nhwc(x3, wf3, b3, relu=True,
+                                                                                     out_dtype=torch.bfloat16),
+                               lambda: F.relu(F.conv2d(x3[:4].permute(0, 3, 1, 2).double(), w3.double(), b3.double())))
+
+lib = _abi.load()
+res = {k: {s: [] for s in SHAPES} for k in layers}
+errs = {k: {} for k in layers}
+for s in SHAPES:  # correctness per shape (and warm-up)
+    lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, s)
+    for k, (flop, fn, ref) in layers.items():
+        out = fn()
+        torch.cuda.synchronize()
+        if ref is not None:
+            r = ref()
+            o = out[:4].double()
+            if o.shape != r.shape:
+                o = o.permute(0, 3, 1, 2)
+            errs[k][s] = float((o - r).abs().max() / (r.abs().max() + 1e-9))
+for rnd_i in range(ROUNDS):
+    for s in SHAPES:
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, s)
+        for k, (flop, fn, ref) in layers.items():
+            res[k][s].append(timeit(fn))
+lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, 16)
+for k, (flop, fn, ref) in layers.items():
+    line = [f"{k:20s} B={B}"]
+    for s in SHAPES:
+        v = sorted(res[k][s])
+        med = v[len(v) // 2]
+        line.append(f"mfma{s}: med {med:.4f} ms min {v[0]:.4f} ({flop / med / 1e12:.3f} PF/s) err {errs[k].get(s, float('nan')):.2e}")
+    print(" | ".join(line), flush=True)

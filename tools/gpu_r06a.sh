@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r06a
 mkdir -p $O
-cd $R && timeout -k 10 900 python -u -m pytest tests/test_gpu_closed_loop.py tests/test_gpu_graph.py tests/test_gpu_learner.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+cd $R && timeout -k 10 900 python -u -m pytest tests/test_gpu_closed_loop.py tests/test_gpu_graph.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 B="python $R/bench.py"
 S="import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c=d.get('closed_loop') or {}; print(sys.argv[2], round(d['value']/1e6,3), round(d['ms_per_step'],4), round(d['roofline']['frac'],4), round(d['hbm_roofline_pct_whole_step'],2), d['config']['graph'] and d['config']['graph']['skewed'], {k: (round(c[k]['value']/1e6,3), round(c[k]['hbm_roofline_pct_whole_step'],2)) for k in ('step_graph','step_plain','policy_graph') if k in c}, round(d['construct_s'],1))"
@@ -21,3 +21,9 @@ for off in 0 57344; do
   timeout -k 10 400 $B --config C4 --envs 8192 --env-offset $off --steps 200 --warmup 20 --cpu-seconds 0 --compact-steps 0 --strong-config none > $O/bench_c4_8192_${off}_200.json 2> $O/bench_c4_8192_${off}_200.err || { tail -20 $O/bench_c4_8192_${off}_200.err; exit 1; }
   python -c "$S" $O/bench_c4_8192_${off}_200.json C4s200_off$off
 done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_conv_mfma.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_conv.log 2>&1 || { tail -40 $O/pytest_conv.log; exit 1; }
+tail -1 $O/pytest_conv.log
+timeout -k 10 300 python -u tools/conv_ab.py 256 7 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
+cat $O/conv_ab.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_learner.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_learner.log 2>&1 || { tail -40 $O/pytest_learner.log; exit 1; }
+tail -1 $O/pytest_learner.log

@@ -174,6 +174,23 @@ struct Mfma<16> {
 };
 
 
+// B fragment (output-channel block nb of MS, k-step s of Mfma<MS>::KS channels) of lane (r, kh) at tap
+// t.  MS = 16 reads w[t][n = nb * 16 + r][s * 32 + 8 kh .. +8]: plain [KH][KW][N][C] at C = 32 is 16
+// rows x 64 bytes = 1 KiB contiguous; in fragment order (WF, laid out for the 32x32x16 operand) the
+// same 8 channels sit at ((t NB + nb / 2) (C / 16) + 2 s) 512 + 256 kh + ((nb & 1) 16 + r) 8: four
+// 256-byte runs
+template <int C, int NB, bool WF, int MS>
+__device__ __forceinline__ bf16x8 load_bfrag_ms(const __bf16* __restrict__ w, int t, int nb, int s, int r, int kh) {
+  if constexpr (MS == 32) {
+    return load_bfrag<C, NB, WF>(w, t, nb, s, r, kh);
+  } else if constexpr (WF) {
+    return *(const bf16x8*)(w + (size_t)((t * NB + (nb >> 1)) * (C / 16) + 2 * s) * 512 + kh * 256 +
+                            ((nb & 1) * 16 + r) * 8);
+  } else {
+    return *(const bf16x8*)(w + ((size_t)(t * NB * 32 + nb * 16 + r) * C + s * 32 + kh * 8));
+  }
+}
+
 template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
@@ -184,7 +201,6 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   constexpr int PT = kWaves * MBW * 32;
   constexpr int AM = MBW * 32 / MS, AN = N / MS;  // MFMA blocks per wave: positions x channels
   constexpr int KSTEPS = C / M::KS;                // k-steps per tap
-  static_assert(!WF || MS == 32, "fragment-order weights are laid out for the 32x32x16 operand");
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const int b = blockIdx.y;
   const int P = Ho * Wo;
@@ -244,10 +260,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
     for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        if constexpr (MS == 32)
-          dst[nb][s] = load_bfrag<C, NB, WF>(w, t, nb, s, r, kh);
-        else  // w [KH][KW][N][C]: row n = nb * 16 + r, channels s * 32 + 8 kh .. +8
-          dst[nb][s] = *(const bf16x8*)(w + ((size_t)(t * N + nb * 16 + r) * C + s * 32 + kh * 8));
+        dst[nb][s] = load_bfrag_ms<C, NB, WF, MS>(w, t, nb, s, r, kh);
       }
   };
   constexpr int kBAhead = FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
@@ -349,18 +362,21 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
 // instead (wave w takes kernel rows ky = w, w + 4, ...), each holding all 4 position blocks x NB
 // channel blocks; the input window of the tile (all its rows for every ky) is staged in LDS once,
 // and the 4 partial accumulators are summed through LDS in the epilogue.
-template <int C, int NB, bool PAD, bool WF>
+template <int C, int NB, bool PAD, bool WF, int MS = 32>
 __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                             const float* __restrict__ bias, void* __restrict__ y,
                                                             int H, int W, int KH, int KW, int pad, int dx, int flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int N = NB * 32, MBW = 4, PT = 128;
+  using M = Mfma<MS>;
+  constexpr int N = NB * 32, PT = 128;
+  constexpr int AM = PT / MS, AN = N / MS;  // MFMA blocks per wave: all 128 positions x all N channels
+  constexpr int KSTEPS = C / M::KS;
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   const int b = blockIdx.y;
   const int P = Ho * Wo;
   const int p0 = blockIdx.x * PT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
+  const int r = lane & (MS - 1), kh = lane / MS;
   const int rowbytes = W * C * 2;
   const int pitch = lds_pitch<C>(W);  // padded row images (cell_off)
   const int2 gin = in_geom<C>(W, dx, flags);
@@ -382,80 +398,77 @@ __global__ __launch_bounds__(256, 2) void conv_small_kernel(const __bf16* __rest
     }
   }
   if (PAD && threadIdx.x < C / 8) *(uint4*)(lds + zero_off + 16 * threadIdx.x) = uint4{0u, 0u, 0u, 0u};
-  int ypos[MBW], xcol[MBW];
+  int ypos[AM], xcol[AM];
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb) {
-    const int m = min(p0 + mb * 32 + r, P - 1);
+  for (int mb = 0; mb < AM; ++mb) {
+    const int m = min(p0 + mb * MS + r, P - 1);
     ypos[mb] = m / Wo - yf - ky_lo;  // window slot of kernel row ky_lo
     xcol[mb] = m % Wo - pad;
   }
   __syncthreads();
 
-  f32x16 acc[MBW][NB];
+  typename M::acc_t acc[AM][AN];
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
+  for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x16{};
+    for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = typename M::acc_t{};
 
   for (int ky = ky_lo + wave; ky <= ky_hi; ky += kWaves) {
-    int aoff[MBW];
+    int aoff[AM];
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb) aoff[mb] = (ypos[mb] + ky) * pitch;
-    bf16x8 bcur[NB][C / 16];
+    for (int mb = 0; mb < AM; ++mb) aoff[mb] = (ypos[mb] + ky) * pitch;
+    bf16x8 bcur[AN][KSTEPS];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-      for (int s = 0; s < C / 16; ++s)
-        bcur[nb][s] = load_bfrag<C, NB, WF>(w, ky * KW, nb, s, r, h);
+      for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = load_bfrag_ms<C, NB, WF, MS>(w, ky * KW, nb, s, r, kh);
     for (int kx = 0; kx < KW; ++kx) {
       const int tn = ky * KW + min(kx + 1, KW - 1);
-      bf16x8 bnext[NB][C / 16];
+      bf16x8 bnext[AN][KSTEPS];
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
+      for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-        for (int s = 0; s < C / 16; ++s)
-          bnext[nb][s] = load_bfrag<C, NB, WF>(w, tn, nb, s, r, h);
-      int abase[MBW];
+        for (int s = 0; s < KSTEPS; ++s) bnext[nb][s] = load_bfrag_ms<C, NB, WF, MS>(w, tn, nb, s, r, kh);
+      int abase[AM];
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) {
+      for (int mb = 0; mb < AM; ++mb) {
         const int col = xcol[mb] + kx * dx;
-        abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + h * 16;
+        abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + kh * 16;
       }
 #pragma unroll
-      for (int s = 0; s < C / 16; ++s) {
-        bf16x8 a[MBW];
+      for (int s = 0; s < KSTEPS; ++s) {
+        bf16x8 a[AM];
 #pragma unroll
-        for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * 32);
+        for (int mb = 0; mb < AM; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
 #pragma unroll
-        for (int mb = 0; mb < MBW; ++mb)
+        for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bcur[nb][s], acc[mb][nb], 0, 0, 0);
+          for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[mb], bcur[nb][s], acc[mb][nb]);
       }
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
+      for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-        for (int s = 0; s < C / 16; ++s) bcur[nb][s] = bnext[nb][s];
+        for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnext[nb][s];
     }
   }
 
   // sum the 4 waves' partials through LDS, one channel block at a time: red[wave][mb][i][lane]
   const bool relu = flags & FFMP_CONV_RELU, out_bf16 = flags & FFMP_CONV_OUT_BF16;
   float* red = (float*)lds;
-  constexpr int E = MBW * 16 * 64;  // entries per wave
+  constexpr int E = AM * M::NACC * 64;  // entries per wave (= 4 * 16 * 64 for either shape)
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
+  for (int nb = 0; nb < AN; ++nb) {
     __syncthreads();  // the window (nb = 0) or the previous block's sums are no longer read
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb)
+    for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[wave * E + (mb * 16 + i) * 64 + lane] = acc[mb][nb][i];
+      for (int i = 0; i < M::NACC; ++i) red[wave * E + (mb * M::NACC + i) * 64 + lane] = acc[mb][nb][i];
     __syncthreads();
     for (int e = threadIdx.x; e < E; e += 256) {
-      const int ln = e & 63, i = (e >> 6) & 15, mb = e >> 10;
-      const int m = p0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * (ln >> 5);
+      const int ln = e & 63, i = (e >> 6) % M::NACC, mb = (e >> 6) / M::NACC;
+      const int m = p0 + mb * MS + M::row(i, ln / MS);
       if (m >= P) continue;
-      const int n = nb * 32 + (ln & 31);
+      const int n = nb * MS + (ln & (MS - 1));
       float v = red[e] + red[E + e] + red[2 * E + e] + red[3 * E + e] + (bias ? bias[n] : 0.f);
       if (relu) v = fmaxf(v, 0.f);
       const size_t o = ((size_t)b * P + m) * N + n;
@@ -482,8 +495,12 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
   const dim3 grid((Ho * Wo + 127) / 128, B);
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF>), grid, dim3(256), lds, s, (const __bf16*)x, (const __bf16*)w,
-                     bias, y, H, W, KH, KW, pad, dx, flags);
+  if (ffmp_detail::g_conv_mfma == 16)
+    hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, flags);
+  else
+    hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF, 32>), grid, dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
   return FFMP_OK;
@@ -527,8 +544,8 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
   if (t_conv_dry) return FFMP_OK;
-  if (!WF && ffmp_detail::g_conv_mfma == 16)
-    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, false, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
+  if (ffmp_detail::g_conv_mfma == 16)
+    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
                        (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32>), grid, dim3(256), lds, s, (const __bf16*)x,

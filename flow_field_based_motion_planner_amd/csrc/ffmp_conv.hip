@@ -863,16 +863,21 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
 // 4 waves x 18 positions at one wave per SIMD (2.64); valid positions two at a time (490 spilled VGPRs).
 constexpr int kDgradNW = 8, kDgradPW = 9, kDgradKQ = 2;  // 72 output columns per row, 2 waves/SIMD
 
-template <int C, int N, int NW, int PW, int KQ>
+template <int C, int N, int NW, int PW, int KQ, int MS = 32>
 __global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16* __restrict__ g,
                                                                  const __bf16* __restrict__ w,
                                                                  void* __restrict__ y, int B, int Hy, int Wy,
                                                                  int KH, int KW, int flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int NB = N / 32;
+  using M = Mfma<MS>;
   constexpr int NQ = C / (16 * KQ);  // phases per kernel row
+  // MFMA blocks per position: samples (32 = AM x MS) x output channels (N = AN x MS); k-steps of
+  // M::KS channels per phase (MS = 16: one of 32 = the phase's KQ = 2 chunks of 16)
+  constexpr int AM = 32 / MS, AN = N / MS, KSTEPS = KQ * 16 / M::KS;
+  static_assert(KSTEPS >= 1 && KQ * 16 % M::KS == 0, "a phase holds whole k-steps");
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
+  const int r = lane & 31, h = lane >> 5;          // the staging lanes: sample r, channel half h
+  const int fr = lane & (MS - 1), fk = lane / MS;  // the operand lanes: row, k-chunk of 8 channels
   const int G = (B + 31) / 32;
   const int rank = blockIdx.x / G, grp = blockIdx.x % G;
   const int padY = KH - 1, padX = KW - 1;
@@ -894,6 +899,12 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16*
     return *(const uint4*)(gs + ((size_t)u * Wy + v) * C * 2 + ((q * KQ + s) * 16 + 8 * h) * 2);
   };
   auto piece_lds = [&](int buf, int p) -> uint4* { return (uint4*)(lds + buf * bufb + p * 1024 + lane * 16); };
+  // the A fragment (samples mb MS + fr, channel chunk kc = 2 k-step-of-16 + half) inside a column:
+  // chunk kc of sample b sits at (kc / 2) 1024 + (kc & 1) 512 + b 16
+  auto a_off = [&](int s, int mb) -> int {
+    const int kc = s * (M::KS / 8) + fk;
+    return (kc >> 1) * 1024 + (kc & 1) * 512 + (mb * MS + fr) * 16;
+  };
 
   {  // phase 0 into buffer 0
     const int u0 = Y + ky_lo - padY;
@@ -901,32 +912,34 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16*
   }
   __syncthreads();
 
-  f32x16 acc[PW][NB];
+  typename M::acc_t acc[PW][AM][AN];
 #pragma unroll
   for (int i = 0; i < PW; ++i)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[i][nb] = f32x16{};
+    for (int mb = 0; mb < AM; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < AN; ++nb) acc[i][mb][nb] = typename M::acc_t{};
 
-  // B fragments of tap t, k-steps q KQ .. +KQ: w [KH][KW][C/8][N][8]: lane (r, h) of k-step ks reads
-  // chunk 2 ks + h, n = nb 32 + r — 1 KiB of consecutive bytes per fragment
-  auto load_b = [&](int t, int q, bf16x8 (&dst)[KQ][NB]) {
+  // B fragments of tap t, the phase's k-steps: w [KH][KW][C/8][N][8]: lane (fr, fk) of k-step ks reads
+  // chunk (q KQ 16 + ks KS) / 8 + fk, n = nb MS + fr — MS x 16 bytes of consecutive memory per chunk
+  auto load_b = [&](int t, int q, bf16x8 (&dst)[KSTEPS][AN]) {
 #pragma unroll
-    for (int s = 0; s < KQ; ++s)
+    for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        dst[s][nb] = *(const bf16x8*)(w + (((size_t)t * (C / 8) + 2 * (q * KQ + s) + h) * N + nb * 32 + r) * 8);
+      for (int nb = 0; nb < AN; ++nb)
+        dst[s][nb] = *(const bf16x8*)(w + (((size_t)t * (C / 8) + (q * KQ * 16 + s * M::KS) / 8 + fk) * N + nb * MS + fr) * 8);
   };
 
   for (int ph = 0; ph < nph; ++ph) {
     const int ky = ky_lo + ph / NQ, q = ph % NQ, buf = ph & 1;
     const bool more = ph + 1 < nph;
     const int u1 = Y + ky_lo + (ph + 1) / NQ - padY, q1 = (ph + 1) % NQ;
-    bf16x8 bcur[KQ][NB];
+    bf16x8 bcur[KSTEPS][AN];
     load_b(ky * KW, q, bcur);
     uint4 pc = uint4{0u, 0u, 0u, 0u};
     int pprev = -1;  // the piece held in pc, written one kernel column later
     for (int j = 0; j < KW; ++j) {
-      bf16x8 bnx[KQ][NB];
+      bf16x8 bnx[KSTEPS][AN];
       load_b(ky * KW + min(j + 1, KW - 1), q, bnx);
       if (more) {
         if (pprev >= 0) *piece_lds(buf ^ 1, pprev) = pc;
@@ -939,24 +952,27 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16*
       const int ilo = t0 <= 0 ? 0 : (t0 + NW - 1) / NW;
       const int t1 = min(padX + Wy - 1 - j, Wx - 1) - wave;
       const int ihi = t1 < 0 ? -1 : min(PW - 1, t1 / NW);
-      const char* abase = lds + buf * bufb + (wave + j - padX) * colb + lane * 16;
+      const char* abase = lds + buf * bufb + (wave + j - padX) * colb;
 #pragma unroll
       for (int i = 0; i < PW; ++i) {
         if (i >= ilo && i <= ihi) {
-          bf16x8 a[KQ];
+          bf16x8 a[KSTEPS][AM];
 #pragma unroll
-          for (int s = 0; s < KQ; ++s) a[s] = *(const bf16x8*)(abase + NW * i * colb + s * 1024);
+          for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
-          for (int s = 0; s < KQ; ++s)
+            for (int mb = 0; mb < AM; ++mb) a[s][mb] = *(const bf16x8*)(abase + NW * i * colb + a_off(s, mb));
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              acc[i][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], bcur[s][nb], acc[i][nb], 0, 0, 0);
+          for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+            for (int mb = 0; mb < AM; ++mb)
+#pragma unroll
+              for (int nb = 0; nb < AN; ++nb) acc[i][mb][nb] = M::mma(a[s][mb], bcur[s][nb], acc[i][mb][nb]);
         }
       }
 #pragma unroll
-      for (int s = 0; s < KQ; ++s)
+      for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) bcur[s][nb] = bnx[s][nb];
+        for (int nb = 0; nb < AN; ++nb) bcur[s][nb] = bnx[s][nb];
     }
     if (more) {
       if (pprev >= 0) *piece_lds(buf ^ 1, pprev) = pc;
@@ -965,24 +981,26 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_dgrad_bm_kernel(const __bf16*
     __syncthreads();
   }
 
-  // epilogue: D row = sample (e & 3) + 8 (e >> 2) + 4 h, column = n (r)
+  // epilogue: D row = sample mb MS + Mfma<MS>::row(e, fk), column = n (fr)
   const bool out_bf16 = flags & FFMP_CONV_OUT_BF16;
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
     const int X = wave + NW * i;
     if (X >= Wx) continue;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (b >= B) continue;
-        const size_t o = (((size_t)b * Hx + Y) * Wx + X) * N + nb * 32 + r;
-        if (out_bf16)
-          ((__bf16*)y)[o] = (__bf16)acc[i][nb][e];
-        else
-          ((float*)y)[o] = acc[i][nb][e];
-      }
+      for (int nb = 0; nb < AN; ++nb)
+#pragma unroll
+        for (int e = 0; e < M::NACC; ++e) {
+          const int b = b0 + mb * MS + M::row(e, fk);
+          if (b >= B) continue;
+          const size_t o = (((size_t)b * Hx + Y) * Wx + X) * N + nb * MS + fr;
+          if (out_bf16)
+            ((__bf16*)y)[o] = (__bf16)acc[i][mb][nb][e];
+          else
+            ((float*)y)[o] = acc[i][mb][nb][e];
+        }
   }
 }
 
@@ -998,8 +1016,12 @@ int launch_dgrad_bm(const void* g, const void* w, void* y, int B, int Hy, int Wy
   const long blocks = (long)Hx * ((B + 31) / 32);
   if (blocks > 0x7fffffffL) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: grid too large");
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
-                     (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
+  if (ffmp_detail::g_conv_mfma == 16)
+    hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ, 16>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
+                       (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
+  else
+    hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ, 32>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
+                       (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d_dgrad launch: %s", hipGetErrorString(e));
   return FFMP_OK;

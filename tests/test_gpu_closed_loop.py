@@ -139,8 +139,9 @@ def test_closed_loop_graph_equals_step_loop(window, seamless, fused):
     for k in range(2):
         a.step(a.policy_reactive())
         b.step(b.policy_reactive())
-    g = a.capture(policy="reactive")
-    assert g.policy == "reactive" and not g.skewed and not g.pipelined
+    per = a.graph_period()
+    g = a.capture(per * -(-8 // per), policy="reactive")  # >= 8 steps: truncations (max_steps 7) inside
+    assert g.policy == "reactive" and not g.skewed and not g.pipelined and g.chainable
     with pytest.raises(ValueError):
         g.replay(torch.zeros((g.steps, n), dtype=torch.int64, device=DEV))
     with pytest.raises(ValueError):

@@ -645,23 +645,26 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
 #ifndef FFMP_WGRAD_PREFETCH
 #define FFMP_WGRAD_PREFETCH 0
 #endif
-template <int C, int N, int TW>
+template <int C, int N, int TW, int MS = 32>
 __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
                                                             float* __restrict__ part, int B, int H, int W, int KH,
                                                             int KW, int dx, int TKY, int TKX, int R, int per_chunk) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int NB = N / 32, CB = C / 32;
+  using M = Mfma<MS>;
+  constexpr int AN = N / MS, AC = C / MS;  // MFMA blocks: output channels (rows) x input channels (columns)
+  constexpr int KP = M::KS;                // positions per k-step (16 or 32)
   const int Ho = H - KH + 1, Wo = W - (KW - 1) * dx;
   const int groups_x = KW / TKX;
   const int kyA = (blockIdx.x / groups_x) * TKY, kxA = (blockIdx.x % groups_x) * TKX;
   const int b0 = blockIdx.y * per_chunk, b1 = min(B, b0 + per_chunk);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int q = (lane & 15) >> 2, pp = lane & 3, gh = (lane >> 4) & 1;  // tr-read: row q, columns 4pp.., half gh
+  const int fr = lane & (MS - 1), fk = lane / MS;       // operand row / k-chunk of 8 positions
+  const int q = (lane & 15) >> 2, pp = lane & 3;        // tr-read: row q of 4, columns 4pp .. of 16
+  const int gh = MS == 32 ? (lane >> 4) & 1 : 0;        // 32x32x16: the 16-column half of the 32
   const int grow = N * 2, xrowb = C * 2;             // image row bytes
   const int Pmax = R * Wo;                            // positions of a full stage
   char* gimg = lds;
-  char* ximg = lds + (Pmax + 16) * grow;              // g image + 16 zero rows (k-steps past the stage end)
+  char* ximg = lds + (Pmax + KP) * grow;              // g image + KP zero rows (k-steps past the stage end)
 
   // this wave's taps of the rectangle (the host makes the rectangle tile the kernel exactly);
   // the B image row of (position row pr, column pc) at tap t: (pr + dky[t]) * W + pc + dkx[t]
@@ -672,20 +675,20 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
     dky[t] = k / TKX;
     dkx[t] = (kxA + k % TKX) * dx;
   }
-  for (int i = threadIdx.x; i < grow; i += 256) *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x; i < grow * KP / 16; i += 256) *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
 
-  f32x16 acc[TW][NB][CB];
+  typename M::acc_t acc[TW][AN][AC];
 #pragma unroll
   for (int t = 0; t < TW; ++t)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-      for (int cb = 0; cb < CB; ++cb) acc[t][nb][cb] = f32x16{};
+      for (int cb = 0; cb < AC; ++cb) acc[t][nb][cb] = typename M::acc_t{};
 
   const int stages_per_sample = (Ho + R - 1) / R;
   const int nstages = (b1 - b0) * stages_per_sample;
   // lane-constant parts of the tr-read addresses
-  const int acol0 = (16 * gh + 4 * pp) * 2;  // + nb * 64 bytes
+  const int acol0 = (16 * gh + 4 * pp) * 2;  // + nb * MS * 2 bytes
   uint4 buf0, buf1, buf2, buf3, buf4, buf5, buf6, buf7, buf8, buf9, buf10, buf11;  // kWgradPieces
   int gq = 0, xq = 0;
   if (nstages > 0) {
@@ -711,26 +714,26 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
       FFMP_WGRAD_LOAD(gs, xs)
     }
     const int Ps = nr * Wo;
-    // this lane's two k rows per k-step (u = 0, 1): position p = k0 + 8h + 4u + q, as (stage
-    // row, column), advanced by 16 per k-step without branches (Wo >= 8: host check)
+    // this lane's two k rows per k-step (u = 0, 1): position p = k0 + 8 fk + 4u + q, as (stage
+    // row, column), advanced by KP per k-step without branches on data (Wo >= 8: host check)
     int pr[2], pc[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int p = 8 * h + 4 * u + q;
+      const int p = 8 * fk + 4 * u + q;
       pr[u] = p / Wo;
       pc[u] = p - pr[u] * Wo;
     }
-    // each operand fragment = two transposing reads (k rows 8h + 4u .. +4), joined as whole
+    // each operand fragment = two transposing reads (k rows 8 fk + 4u .. +4), joined as whole
     // vectors (element-wise assembly of the 4 x 16-bit results miscompiles: ROCm 7.2)
-    auto fetch = [&](int k0, s16x4 (&ar)[NB][2], s16x4 (&br)[TW][CB][2]) {
+    auto fetch = [&](int k0, s16x4 (&ar)[AN][2], s16x4 (&br)[TW][AC][2]) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int p = k0 + 8 * h + 4 * u + q;
+        const int p = k0 + 8 * fk + 4 * u + q;
         const bool in = p < Ps;
-        const int grw = in ? p : Pmax + (p & 15);  // past the stage end: a zero row
+        const int grw = in ? p : Pmax + (p & (KP - 1));  // past the stage end: a zero row
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const int col = acol0 + nb * 64;
+        for (int nb = 0; nb < AN; ++nb) {
+          const int col = acol0 + nb * MS * 2;
           const int off = N == 64 ? ((col & ~15) ^ swz128(grw)) | (col & 15) : col;
           ar[nb][u] = tr_read(gimg + grw * grow + off);
         }
@@ -739,73 +742,74 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
         for (int t = 0; t < TW; ++t) {
           const int xrw = base + dky[t] * W + dkx[t];
 #pragma unroll
-          for (int cb = 0; cb < CB; ++cb) {
-            const int col = acol0 + cb * 64;
+          for (int cb = 0; cb < AC; ++cb) {
+            const int col = acol0 + cb * MS * 2;
             const int off = C == 64 ? ((col & ~15) ^ swz128(xrw)) | (col & 15) : col;
             br[t][cb][u] = tr_read(ximg + xrw * xrowb + off);
           }
         }
-        int c = pc[u] + 16, rr = pr[u];
-        if (c >= Wo) c -= Wo, ++rr;
-        if (c >= Wo) c -= Wo, ++rr;
+        int c = pc[u] + KP, rr = pr[u];
+#pragma unroll
+        for (int wrap = 0; wrap < KP / 8; ++wrap)
+          if (c >= Wo) c -= Wo, ++rr;
         pc[u] = c;
         pr[u] = rr;
       }
     };
-    auto mma = [&](const s16x4 (&ar)[NB][2], const s16x4 (&br)[TW][CB][2]) {
-      bf16x8 a[NB], bb[TW][CB];
+    auto mma = [&](const s16x4 (&ar)[AN][2], const s16x4 (&br)[TW][AC][2]) {
+      bf16x8 a[AN], bb[TW][AC];
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
+      for (int nb = 0; nb < AN; ++nb)
         a[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ar[nb][0], ar[nb][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
+        for (int cb = 0; cb < AC; ++cb)
           bb[t][cb] = __builtin_bit_cast(bf16x8,
                                          __builtin_shufflevector(br[t][cb][0], br[t][cb][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
+        for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-          for (int cb = 0; cb < CB; ++cb)
-            acc[t][nb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[nb], bb[t][cb], acc[t][nb][cb], 0, 0, 0);
+          for (int cb = 0; cb < AC; ++cb) acc[t][nb][cb] = M::mma(a[nb], bb[t][cb], acc[t][nb][cb]);
     };
-    constexpr bool kPrefetch = FFMP_WGRAD_PREFETCH < 0 ? TW * NB * CB >= 16 : FFMP_WGRAD_PREFETCH != 0;
+    constexpr bool kPrefetch = FFMP_WGRAD_PREFETCH < 0 ? TW * AN * AC * (MS / 16) * (MS / 16) >= 64
+                                                       : FFMP_WGRAD_PREFETCH != 0;
     if constexpr (kPrefetch) {
       // the next k-step's fragments are read while this one's MFMAs run (two register sets, the loop
       // unrolled by two so they swap roles without copies)
-      s16x4 arA[NB][2], brA[TW][CB][2], arB[NB][2], brB[TW][CB][2];
+      s16x4 arA[AN][2], brA[TW][AC][2], arB[AN][2], brB[TW][AC][2];
       fetch(0, arA, brA);
-      for (int k0 = 0; k0 < Ps; k0 += 32) {
-        fetch(k0 + 16, arB, brB);
+      for (int k0 = 0; k0 < Ps; k0 += 2 * KP) {
+        fetch(k0 + KP, arB, brB);
         mma(arA, brA);
-        if (k0 + 16 >= Ps) break;
-        fetch(k0 + 32, arA, brA);
+        if (k0 + KP >= Ps) break;
+        fetch(k0 + 2 * KP, arA, brA);
         mma(arB, brB);
       }
     } else {
-      for (int k0 = 0; k0 < Ps; k0 += 16) {
-        s16x4 ar[NB][2], br[TW][CB][2];
+      for (int k0 = 0; k0 < Ps; k0 += KP) {
+        s16x4 ar[AN][2], br[TW][AC][2];
         fetch(k0, ar, br);
         mma(ar, br);
       }
     }
   }
 
-  // partial sums: part[chunk][tap][n][c]; C/D row = n ((i & 3) + 8 (i >> 2) + 4 h), column = c (r)
+  // partial sums: part[chunk][tap][n][c]; C/D row = n (nb MS + Mfma<MS>::row(i, fk)), column = c (fr)
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     const int k = wave * TW + t;
     float* dst = part + ((size_t)blockIdx.y * KH * KW + (kyA + k / TKX) * KW + kxA + k % TKX) * N * C;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-      for (int cb = 0; cb < CB; ++cb)
+      for (int cb = 0; cb < AC; ++cb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int n = nb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          dst[n * C + cb * 32 + r] = acc[t][nb][cb][i];
+        for (int i = 0; i < M::NACC; ++i) {
+          const int n = nb * MS + M::row(i, fk);
+          dst[n * C + cb * MS + fr] = acc[t][nb][cb][i];
         }
   }
 }
@@ -818,8 +822,9 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   const int TKX = std::min(KW, TG), TKY = TG / TKX;
   if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
   // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
+  const int ms = ffmp_detail::g_conv_mfma == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
   int R = std::min(Ho, 8);
-  auto bytes = [&](int rr) { return (size_t)(rr * Wo + 16) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
+  auto bytes = [&](int rr) { return (size_t)(rr * Wo + kp) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
   auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };
   while (R > 1 && (bytes(R) > 48 * 1024 || pieces(R) > kWgradPieces * 256)) --R;
   if (bytes(R) > 64 * 1024 || pieces(R) > kWgradPieces * 256)
@@ -828,8 +833,12 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   const int per_chunk = (B + chunks - 1) / chunks;
   const dim3 grid((KH / TKY) * (KW / TKX), (B + per_chunk - 1) / per_chunk);
   if (t_conv_dry) return FFMP_OK;
-  hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW>), grid, dim3(256), bytes(R), s, (const __bf16*)g, (const __bf16*)x,
-                     part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+  if (ms == 16)
+    hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 16>), grid, dim3(256), bytes(R), s, (const __bf16*)g,
+                       (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 32>), grid, dim3(256), bytes(R), s, (const __bf16*)g,
+                       (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d_wgrad launch: %s", hipGetErrorString(e));
   return FFMP_OK;

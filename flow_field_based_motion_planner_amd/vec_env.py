@@ -1312,7 +1312,7 @@ class FFMPVec:
     INFO_FORMATS = ("dict", "list")
 
     def _info_list(self) -> tuple:
-        keys = ("is_goal", "collision", "truncated", "step", "episode")
+        keys = ("is_goal", "collision", "truncated", "t", "episode")  # info key "step" is the counter t
         cols = torch.stack([getattr(self, k).to(torch.int64) for k in keys]).cpu().tolist()
         return tuple({"is_goal": bool(g), "collision": bool(c), "truncated": bool(tr), "step": int(st),
                       "episode": int(ep)} for g, c, tr, st, ep in zip(*cols))

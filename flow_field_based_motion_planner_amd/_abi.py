@@ -134,6 +134,7 @@ _SIGS = {
     "ffmp_ring_rebuild": (C.c_int, [_P, C.c_uint64, _P, _I64, C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "ffmp_ring_destroy": (C.c_int, [_P]),
     "ffmp_ring_pool_bytes": (_I64, [_I32]),
+    "ffmp_ring_va_reserved": (_I64, [_I32]),
     "ffmp_ring_pool_trim": (C.c_int, [_I32, _I64, C.POINTER(_I64)]),
     "ffmp_ring_pair_forget": (C.c_int, [_I32, _P]),
     "ffmp_ring_pair_refs": (C.c_int, [_I32]),

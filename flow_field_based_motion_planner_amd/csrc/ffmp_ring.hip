@@ -18,6 +18,12 @@ int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_e
 
 // FFMP_TUNE_RING_EXTRA: fresh pieces beyond need per create / rebuild (0 = default, v = cap v - 1)
 std::atomic<int32_t> g_ring_extra{0};
+// bytes of virtual address space reserved so far per device (never freed: see ffmp_ring_va_reserved)
+constexpr int kVaDevices = 64;
+std::atomic<int64_t> g_va_reserved[kVaDevices];
+void note_va(int32_t device, size_t bytes) {
+  if (device >= 0 && device < kVaDevices) g_va_reserved[device].fetch_add((int64_t)bytes);
+}
 int32_t ring_extra_swap(int32_t v) { return g_ring_extra.exchange(v); }
 }
 using ffmp_detail::fail;
@@ -193,6 +199,7 @@ hipError_t new_piece(int32_t device, size_t bytes, size_t gran, ffmp_piece* out)
     (void)hipMemRelease(p.h);  // never mapped: safe to give back
     return e;
   }
+  ffmp_detail::note_va(device, bytes);
   if ((e = map_rw(p.home, bytes, p.h, device)) != hipSuccess) {
     // The reservation is kept (never freed): an address range that was mapped once must not be
     // handed out again, or the runtime can resolve later accesses there to this allocation.
@@ -472,6 +479,7 @@ int ring_map(ffmp_ring* r, const RingGeom& g) {
   // aligned to the piece (up to 1 GiB) so that every piece maps with the largest page fragments
   hipError_t e = hipMemAddressReserve((void**)&r->va, r->vbytes, va_align(g.piece, g.gran), nullptr, 0);
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_ring: hipMemAddressReserve: %s", hipGetErrorString(e));
+  ffmp_detail::note_va(r->device, r->vbytes);
   for (int v = 0; v <= r->slots; ++v) {
     const int slot = v % r->slots;
     for (int j = 0; j < g.per_slot; ++j) {
@@ -593,6 +601,11 @@ int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap) {
   if (cap < 6) return 5;
   out[5] = (double)ring->scale;
   return 6;
+}
+
+int64_t ffmp_ring_va_reserved(int32_t device) {
+  if (device < 0 || device >= ffmp_detail::kVaDevices) return fail(FFMP_E_ARG, "ffmp_ring_va_reserved: device out of range");
+  return ffmp_detail::g_va_reserved[device].load();
 }
 
 int64_t ffmp_ring_pool_bytes(int32_t device) {

@@ -109,19 +109,23 @@ class FFMP(GymEnvBase):
             self._device = torch.device("cuda", torch.cuda.current_device())
         return torch.device(self._device)
 
-    def _legacy_cfg(self, grid: int):
-        """ctypes cfg for the legacy kernels: the footprint of THIS instance's map
-        attributes (ffmp.py:87-94 reads self.map_grid_num / map_grid_size / map_range
-        / robot_rsize) as absolute cells, re-centred on the given map's width.  The reference
-        rebuilds the footprint over all G^2 cells on every call; here it is built once per
-        (attributes, map width) and cached (the attributes are public and may be changed)."""
-        key = (grid, self.map_grid_num, self.map_grid_size, self.map_range, self.robot_rsize, id(self.cfg))
+    def _legacy_cfg(self, shape):
+        """(ctypes cfg, checked cells, complete) for the legacy kernels and a local map of `shape`
+        (H, W).  The footprint is THIS instance's (ffmp.py:87-94 reads self.map_grid_num /
+        map_grid_size / map_range / robot_rsize): ABSOLUTE cells (i, j) in the reference's list order,
+        indexed into the given map as local_map_info[i, j] (ffmp.py:97-101) — whatever the map's
+        width, and whether or not it equals map_grid_num.  The reference raises IndexError at the
+        first cell outside the map that its loop reaches before a hit: the kernel checks the cells
+        before that one (complete = False) and the caller raises when none of them is occupied.  The
+        map is staged into a square plane of side `grid` (max(H, W) rounded up to the kernels' multiple
+        of 4, >= 8; the padding is never read).  Built once per (attributes, shape) and cached (the
+        reference rebuilds the list over all cells on every call; the attributes are public)."""
+        H, W = int(shape[0]), int(shape[1])
+        key = (H, W, self.map_grid_num, self.map_grid_size, self.map_range, self.robot_rsize, id(self.cfg))
         hit = self._cfg_cache.get(key)
-        if hit is not None and hit[2] is self.cfg:  # (a config is replaced, never mutated: FFMPConfig.replace)
+        if hit is not None and hit[3] is self.cfg:  # (a config is replaced, never mutated: FFMPConfig.replace)
             self.robot_grids = hit[1]
-            return hit[0]
-        if grid % 4 or grid < 8:
-            raise ValueError(f"local map width must be a multiple of 4 and >= 8, got {grid}")
+            return hit[0], hit[2]
         cells = []
         half = 0.5 * self.map_range
         for i in range(self.map_grid_num):
@@ -133,18 +137,38 @@ class FFMP(GymEnvBase):
                 if math.sqrt(xp + yp) <= self.robot_rsize:
                     cells.append((i, j))
         self.robot_grids = [np.array([i, j]) for i, j in cells]
+        k_oor = next((k for k, (i, j) in enumerate(cells) if i >= H or j >= W), len(cells))
+        checked = cells[:k_oor]
+        if len(checked) > _abi.MAX_FOOT:
+            raise ValueError(f"the footprint has {len(checked)} cells; the kernels take at most {_abi.MAX_FOOT}")
+        grid = max(8, -(-max(H, W) // 4) * 4)
         cfg = self.cfg.replace(grid=grid, n_beams=0, n_obst=0)
         c = _abi.make_cfg(cfg)
-        c.n_foot = len(cells)
-        for k, (i, j) in enumerate(cells):
-            c.foot_di[k], c.foot_dj[k] = i - grid // 2, j - grid // 2
+        c.n_foot = len(checked)
+        for k, (i, j) in enumerate(checked):
+            c.foot_di[k], c.foot_dj[k] = i - grid // 2, j - grid // 2  # the kernel reads grid/2 + offset = i
         # the lidar threshold: is_collision2 compares with the module constant ROBOT_RSIZE
         # (ffmp.py:112), not with self.robot_rsize (which only shapes the footprint above)
         c.robot_r = float(ROBOT_RSIZE)
         if len(self._cfg_cache) >= 64:
             self._cfg_cache.clear()
-        self._cfg_cache[key] = (c, self.robot_grids, self.cfg)
-        return c
+        complete = k_oor == len(cells)
+        self._cfg_cache[key] = ((c, complete), self.robot_grids, complete, self.cfg)
+        return c, complete
+
+    @staticmethod
+    def _map2d(local_map):
+        """local_map_info as the 2-D plane the reference's [i, j] indexing reads: (H, W) or (H, W, 1);
+        more channels make `local_map_info[i, j] > 0` an array whose truth value is ambiguous."""
+        m = np.asarray(local_map)
+        if m.ndim == 3:
+            if m.shape[2] != 1:
+                raise ValueError("The truth value of an array with more than one element is ambiguous "
+                                 f"(local_map of shape {m.shape}: ffmp.py:101 tests local_map_info[i, j] > 0)")
+            m = m[:, :, 0]
+        if m.ndim != 2:
+            raise ValueError(f"local_map must be (H,W) or (H,W,1), got {np.shape(local_map)}")
+        return m
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -169,16 +193,13 @@ class FFMP(GymEnvBase):
     def _reward_done(self, rel_goal, is_first: bool, d0: float, scan=None, local_map=None,
                      collide_in=None, goal_in=None):
         lib = _abi.load()
-        grid = self.cfg.grid
         m = None
+        shape = (self.cfg.grid, self.cfg.grid)
         if local_map is not None:
-            m = np.asarray(local_map)
-            if m.ndim == 3:
-                m = m[:, :, 0]
-            if m.ndim != 2 or m.shape[0] != m.shape[1]:
-                raise ValueError(f"local_map must be (G,G) or (G,G,1), got {np.shape(local_map)}")
-            grid = m.shape[0]
-        cfg_c = self._legacy_cfg(grid)
+            m = self._map2d(local_map)
+            shape = m.shape
+        cfg_c, complete = self._legacy_cfg(shape)
+        grid = cfg_c.grid
         # the scan as float64: None (the reference's list head, src/train.py:97) -> NaN, which like
         # None and 0.0 never counts as a hit (`bool(r) and r < 0.13`, ffmp.py:112: NaN < 0.13 is false)
         vals = None if scan is None else np.asarray(scan, dtype=np.float64).reshape(-1)
@@ -192,7 +213,10 @@ class FFMP(GymEnvBase):
         if L:
             hnp[48:48 + 8 * L].view(np.float64)[:] = vals
         if m is not None:
-            hnp[moff:nbytes].view(np.float32).reshape(grid, grid)[:] = m
+            plane = hnp[moff:nbytes].view(np.float32).reshape(grid, grid)
+            if m.shape != (grid, grid):
+                plane[:] = 0.0  # the padding (never read: every checked cell lies inside the map)
+            plane[:m.shape[0], :m.shape[1]] = m
         flags = (0 if collide_in is None else 1) | (0 if goal_in is None else 2) | (0 if m is None else 4)
         if m is None and L <= _abi.PACKED_ARG_BEAMS and self.PACKED_ARGS:
             flags |= 8  # inputs as kernel arguments, outputs straight into the pinned block
@@ -201,15 +225,15 @@ class FFMP(GymEnvBase):
                                                flags, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
                    "ffmp_reward_done_packed")
         r, d0n = hnp[0:16].view(np.float64)
+        if m is not None and not complete and not hnp[18]:
+            # no occupied cell before the first one outside the map: the reference's loop reaches it
+            raise IndexError(f"footprint cell outside the local map of shape {tuple(m.shape)} (ffmp.py:101)")
         return float(r), float(d0n), bool(hnp[16]), bool(hnp[17]), bool(hnp[18])
 
     # ---------------------------------------------------- reference methods
     def is_collision(self, local_map_info) -> bool:
-        m = np.asarray(local_map_info)
-        if m.ndim == 3:
-            m = m[:, :, 0]
         # the footprint test alone: one packed ffmp_reward_done call with the map and no scan
-        return self._reward_done((1.0, 0.0), True, 0.0, local_map=m)[4]
+        return self._reward_done((1.0, 0.0), True, 0.0, local_map=local_map_info)[4]
 
     def is_collision2(self, scan_data) -> bool:
         vals = np.asarray(scan_data, dtype=np.float64).reshape(-1)  # None -> NaN: never a hit, as None

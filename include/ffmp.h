@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FFMP_ABI_VERSION 8  /* 8: ffmp_step_skewed_check, ffmp_policy_reactive */
+#define FFMP_ABI_VERSION 8  /* 8: ffmp_step_skewed_check, ffmp_policy_reactive, ffmp_ring_va_reserved */
 #define FFMP_MAX_OBST 64     /* K  */
 #define FFMP_MAX_FOOT 128    /* footprint cells */
 #define FFMP_MAX_BEAMS 1024  /* L  */
@@ -525,6 +525,12 @@ int ffmp_ring_rebuild(ffmp_ring_t* old, uint64_t replace_mask, const void* partn
 int ffmp_ring_destroy(ffmp_ring_t* ring);
 int ffmp_ring_info(const ffmp_ring_t* ring, double* out, int32_t cap);
 int64_t ffmp_ring_pool_bytes(int32_t device);
+/* Bytes of virtual address space the ring helper has reserved on `device` in this process (piece
+ * home mappings + every ring's (slots + 1) virtual slots).  Reservations are never freed while the
+ * process lives (the re-map hazard above), so this only grows: a process that builds and drops rings
+ * in a loop runs out of GPU virtual address space after roughly (device VA) / (per-ring delta)
+ * rebuilds (INTEGRATION.md §5 states the bound measured for C3).  FFMP_E_ARG for device < 0 or >= 64. */
+int64_t ffmp_ring_va_reserved(int32_t device);
 /* Give back the physical memory of pooled pieces of `device` beyond the first keep_bytes
  * (0: all of them): after a device synchronize (pieces of rings dropped while kernels may still
  * write them are drained first), every mapping of such a piece — its home mapping and the slots

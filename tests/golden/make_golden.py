@@ -7,7 +7,8 @@ INPUTS and OUTPUTS only; no reference source is copied into this repository.
 
 What is driven (reference file:line):
   * gym_ffmp.envs.ffmp.FFMP  (src/gym_ffmp/envs/ffmp.py:22-188)
-      is_collision (:85-105), is_collision2 (:108-117), is_goal (:120-127),
+      is_collision (:85-105; also at map widths that are not multiples of 4, differ from
+      map_grid_num or are not square), is_collision2 (:108-117), is_goal (:120-127),
       reward_calculator (:130-157, incl. the module-global d0 and the
       NameError before the first is_first), is_done (:160-164),
       rewarder (:167-176), rewarder2 (:179-188)
@@ -424,6 +425,44 @@ def main():
             r["done_out"], prev = r["episode"] != prev, r["episode"]
         ep["scenarios"].append({"name": name, "max_steps": max_steps, "armed": True, "env_like": True, "rows": rows})
     out["episode_bookkeeping"] = ep
+
+    # ---- is_collision at the edges: map widths that are not multiples of 4 or
+    # differ from map_grid_num, non-square maps, and instance attributes that move the footprint.
+    # The reference indexes the ABSOLUTE cells of its footprint list (ffmp.py:87-101), in list order,
+    # breaking at the first occupied one: a cell outside the given map raises IndexError only when it
+    # is reached before a hit.  Own RNG: the draws above are unchanged.
+    erng = np.random.default_rng(20261018)
+    edge, emaps = [], {}
+    cases = [  # (instance map_grid_num or None = default, map shape)
+        (None, (50, 50)), (None, (98, 98)), (None, (99, 99)), (None, (100, 60)), (None, (60, 100)),
+        (None, (53, 53)), (None, (101, 101)), (64, (100, 100)), (64, (37, 37)), (128, (100, 100)),
+        (128, (66, 66)), (40, (50, 50)),
+    ]
+    for ci, (mg, shape) in enumerate(cases):
+        e = FFMP()
+        if mg is not None:
+            e.map_grid_num = mg
+            e.map_range = mg * ffmp_mod.MAP_RESOLUTION
+        e.is_collision(np.zeros((120, 120), dtype=np.int32))  # the footprint cells of these attributes
+        cells = [(int(c[0]), int(c[1])) for c in e.robot_grids]
+        for k in range(12):
+            m = np.zeros(shape, dtype=np.int32)
+            if k % 3 == 1:  # one occupied footprint cell that lies inside the map, if any
+                inside = [c for c in cells if c[0] < shape[0] and c[1] < shape[1]]
+                if inside:
+                    c = inside[int(erng.integers(0, len(inside)))]
+                    m[c] = int(erng.integers(1, 256))
+            elif k % 3 == 2:  # random clutter
+                m = (erng.random(shape) < 0.08).astype(np.int32) * erng.integers(1, 256, shape).astype(np.int32)
+            try:
+                res = bool(e.is_collision(m))
+            except IndexError:
+                res = "IndexError"
+            key = f"edge_{ci}_{k}"
+            emaps[key] = m.astype(np.uint8)
+            edge.append({"map": key, "map_grid_num": mg, "shape": list(shape), "result": res})
+    out["is_collision_edge"] = edge
+    maps.update(emaps)
 
     with open(os.path.join(OUT_DIR, "ref_pinned.json"), "w") as f:
         json.dump(out, f, indent=0, allow_nan=True)

@@ -13,6 +13,20 @@ from flow_field_based_motion_planner_amd.vec_env import FFMPVec
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture
+def empty_pool():
+    """Order independence: every instance an earlier test dropped is collected
+    and its ring's parked pieces are released, so this test's instance starts from an empty pool."""
+    import gc
+    from flow_field_based_motion_planner_amd import _abi
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    _abi.ring_pool_trim(0, 0)
+    assert _abi.load().ffmp_ring_pool_bytes(0) == 0
+    yield
+
+
 def test_c3_within_budget_beside_a_learner():
     budget = 48 << 30
     env = FFMPVec(32768, preset("C3", seed=3), device="cuda:0", hbm_budget=budget)
@@ -44,7 +58,7 @@ def test_c3_within_budget_beside_a_learner():
     lenv.close()
 
 
-def test_default_c3_parks_no_hbm():
+def test_default_c3_parks_no_hbm(empty_pool):
     """With default arguments the metric's instance holds what it uses: the pairing candidates it did
     not choose and the rings its relocation / repair dropped are released after construction
     (ffmp_ring_pool_trim), so the device's HBM in use grows by at most 10 % more than hbm_bytes()
@@ -59,13 +73,43 @@ def test_default_c3_parks_no_hbm():
     grew, held = free0 - free1, env.hbm_bytes()
     assert env.ring == "seamless" and env.frame_window == 8
     assert grew - held <= 0.10 * held, (grew, held, env.ring_meta)
-    # it did pair: the first 12 positions are always probed (ffmp_ring.hip choose_pieces).  Not
-    # pieces_new >= 64: a ring an earlier test in this process dropped without close() may still be
-    # retired here, and its pieces are legitimately reused as candidates (seen once: 21 new of 64)
-    assert env._ring.info()["pair_probes"] >= 12
+    # it did pair: the first 12 positions are always probed (ffmp_ring.hip choose_pieces); and with
+    # the pool empty at the start (empty_pool) all 64 of its pieces are fresh ones
+    info = env._ring.info()
+    assert info["pair_probes"] >= 12 and info["pieces_new"] >= 64, info
     env.reset()
     env.step(torch.zeros(32768, dtype=torch.int64, device="cuda:0"))
     env.close()
     torch.cuda.synchronize()
     free2, _ = torch.cuda.mem_get_info(0)
     assert free0 - free2 <= 0.02 * held, (free0, free2, held)
+
+
+def test_rebuild_c3_ten_times(empty_pool):
+    """Build and close the metric's instance 10 times in one process: HBM goes back every time, and
+    the virtual address space the frame ring reserves (never freed, include/ffmp.h
+    ffmp_ring_va_reserved) grows by a bounded amount per instance — recorded for INTEGRATION.md §5's
+    per-process rebuild bound."""
+    import gc
+    from flow_field_based_motion_planner_amd import _abi
+    lib = _abi.load()
+    torch.cuda.synchronize()
+    free0, total = torch.cuda.mem_get_info(0)
+    va = [lib.ffmp_ring_va_reserved(0)]
+    for k in range(10):
+        env = FFMPVec(32768, preset("C3", seed=20 + k), device="cuda:0", autotune=False)
+        assert env.ring == "seamless"
+        held = env.hbm_bytes()
+        env.reset()
+        env.step(torch.zeros(32768, dtype=torch.int64, device="cuda:0"))
+        env.close()
+        del env
+        gc.collect()
+        torch.cuda.synchronize()
+        free, _ = torch.cuda.mem_get_info(0)
+        va.append(lib.ffmp_ring_va_reserved(0))
+        print(f"rebuild {k}: HBM not returned {free0 - free} B of {held}; VA reserved +{va[-1] - va[-2]} B "
+              f"(total {va[-1]})", flush=True)
+        assert free0 - free <= 0.02 * held, (k, free0, free, held)
+    per = [b - a for a, b in zip(va, va[1:])]
+    assert all(p > 0 for p in per) and max(per) <= 4 * 80 * 2 ** 30, per

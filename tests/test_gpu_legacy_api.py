@@ -43,6 +43,36 @@ def test_is_collision_random_maps(golden, golden_maps, ffmp):
         assert ffmp.is_collision(m[:, :, None]) == w3d
 
 
+def test_is_collision_edges(golden, golden_maps):
+    """map widths that are not multiples of 4 (50, 98, 99, 53, 101, 37, 66) or
+    differ from map_grid_num, non-square maps, and instance attributes that move the footprint —
+    the absolute cells of ffmp.py:87-101 in list order, IndexError where the reference's loop
+    reaches a cell outside the map before a hit (golden vectors from the reference itself), through
+    the HIP is_collision and rewarder."""
+    for case in golden["is_collision_edge"]:
+        envmod._reset_global_d0()
+        e = envmod.FFMP()
+        if case["map_grid_num"] is not None:
+            e.map_grid_num = case["map_grid_num"]
+            e.map_range = case["map_grid_num"] * 0.05
+        m = golden_maps[case["map"]].astype(np.int32)
+        assert list(m.shape) == case["shape"]
+        want = case["result"]
+        if want == "IndexError":
+            with pytest.raises(IndexError):
+                e.is_collision(m)
+            with pytest.raises(IndexError):
+                e.rewarder(m[:, :, None], np.array([2.0, 0.1]), True)
+            assert envmod._PRE_RELATIVE_GOAL_DIST is None  # raised before the reward, as the reference
+        else:
+            assert e.is_collision(m) == want, case
+            assert e.is_collision(m[:, :, None]) == want, case
+            r, done = e.rewarder(m, np.array([2.0, 0.1]), True)
+            assert done == want and r == (-1.05 if want else -0.05), case
+    with pytest.raises(ValueError):
+        envmod.FFMP().is_collision(np.zeros((100, 100, 2), dtype=np.int32))
+
+
 def test_is_collision2_and_banner(golden, ffmp):
     for case in golden["is_collision2"]:
         buf = io.StringIO()

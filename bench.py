@@ -77,7 +77,7 @@ def parse():
                         "raster kernels, their bytes).  off: one step() call per step")
     p.add_argument("--graph-skew", default="auto", choices=["auto", "on", "off"],
                    help="with --graph on: replay graphs whose steps are ONE launch each (the raster of step i + the "
-                        "env step of step i + 1, ffmp_step_skewed) — auto: time both graphs (3 alternating replays "
+                        "env step of step i + 1, ffmp_step_skewed; open loop: actions known a step ahead) — auto: time both graphs (8 alternating replays "
                         "each, untimed) and keep the faster; on / off: force")
     p.add_argument("--closed-loop", type=int, default=1,
                    help="1 (default): after the open-loop timing, time the main leg closed-loop too (each step's "
@@ -400,14 +400,15 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
             can_skew = StepGraph.skew_supported(env, per0) and args.graph_skew != "off"
             graph = env.capture(skewed=bool(can_skew and args.graph_skew == "on"))
             if can_skew and args.graph_skew == "auto":
-                # the skewed graph (one launch per step) against the two-launch one: 3 alternating
+                # the skewed graph (one launch per step) against the two-launch one: 8 alternating
                 # replays each after one warm replay, the faster (median) kept (C2: the env waves hide
-                # beside the raster; C3: 2,048 env blocks dispatched first delay the raster's stores)
+                # beside the raster; C3: 2,048 env blocks dispatched first delay the raster's stores).
+                # Open loop only: a skewed step needs step i + 1's actions before step i's observation
                 gs = env.capture(skewed=True)
                 ms = {False: [], True: []}
                 for g in (graph, gs):
                     g.replay(actions[:per0])
-                for _ in range(3):
+                for _ in range(8):
                     for key, g in ((False, graph), (True, gs)):
                         a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         a0.record()
@@ -415,7 +416,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
                         a1.record()
                         torch.cuda.synchronize()
                         ms[key].append(a0.elapsed_time(a1))
-                med = {key: sorted(v)[1] for key, v in ms.items()}
+                med = {key: sorted(v)[len(v) // 2] for key, v in ms.items()}
                 chosen = med[True] < 0.995 * med[False]
                 skew_trial = {"chosen": chosen, "serial_replay_ms": [round(v, 4) for v in ms[False]],
                               "skewed_replay_ms": [round(v, 4) for v in ms[True]]}
@@ -441,6 +442,18 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
             graph_rem.replay(actions[:rem])
             for k in range(rem, per):
                 env.step(actions[k])
+        # re-warm: the captures above (torch.cuda.graph synchronizes, collects garbage and empties the
+        # cache) leave the GPU idle for a while, and after an idle gap the first few ms of steps run slow
+        # (profiles/r03b_transient*.txt) — at the 8-GPU strong leg's 0.6-ms steps the driver's 20 timed
+        # steps fell to 0.80 of the roofline from 0.90 at 200 (profiles/r06a_bench_c4_8192_*.json).  Replay
+        # the graph for >= 30 ms of GPU work (untimed, the warm-up's actions) right before the timed region.
+        t_one = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t_one[0].record()
+        graph.replay(actions[:per])
+        t_one[1].record()
+        torch.cuda.synchronize()
+        for _ in range(max(1, int(30.0 / max(t_one[0].elapsed_time(t_one[1]), 1e-3)))):
+            graph.replay(actions[:per])
         torch.cuda.synchronize()
     ep0_t = env.episode.sum()  # read after the loop: no host round trip between the sync and the loop
     if world > 1:
@@ -500,7 +513,7 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
                               world, dev, args.dist_backend)
     closed = None
     if main_leg and args.closed_loop and env.pipeline_slices == 1:
-        closed = closed_loop_leg(env, K, W, world, dev, args.dist_backend, b["total"])
+        closed = closed_loop_leg(env, K, W, world, dev, args.dist_backend, b["total"], el_local * 1e3 / K)
     el = max(r[0] for r in per_rank)  # == the max-reduce over ranks
     n_total = int(sum(r[2] for r in per_rank))
     out = {
@@ -543,7 +556,8 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
     return out, env
 
 
-def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_bytes: float) -> dict:
+def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_bytes: float,
+                    step_ms: float) -> dict:
     """Closed loop (src/train.py:572-577, 665-682: each action is chosen from the previous
     observation, never known a step ahead): step k + 1's actions come from step k's observation on
     the device (FFMPVec.policy_reactive, include/ffmp.h ffmp_policy_reactive: reads state_g and the
@@ -552,10 +566,13 @@ def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_
                    single-step HIP graph (FFMPVec.use_graphs);
       step_plain   the same loop with plain launches;
       policy_graph the policy captured inside a graph of graph_period() steps (capture(policy=...)),
-                   replayed with no host work between steps (the K % period rest: step_graph steps)."""
+                   replayed with no host work between steps (the K % period rest: step_graph steps).
+    Each form's timed region follows >= 30 ms of its own untimed steps (the GPU-idle transient)."""
+    import math
     import torch
     import torch.distributed as dist
     n = env.num_envs
+    warm = max(warm, int(math.ceil(30.0 / max(step_ms, 1e-3))))
     out = {"policy": "ffmp_policy_reactive (scripted controller; reads state_g and the newest frame)",
            "steps": K}
 
@@ -575,7 +592,8 @@ def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_
             env.step(env.policy_reactive(out=env.action_buffer))
 
     env.use_graphs(True)
-    step_loop(max(warm, env.graph_period() + 1))  # every ring position's graph captured and warm
+    step_loop(env.graph_period() + 1)  # every ring position's graph captured ...
+    step_loop(warm)                     # ... then warm
     el = {"step_graph": timed(lambda: step_loop(K))}
     env.use_graphs(False)
     step_loop(warm)
@@ -583,7 +601,8 @@ def closed_loop_leg(env, K: int, warm: int, world: int, dev, backend: str, step_
     env.use_graphs(True)
     per = env.graph_period()
     pg = env.capture(policy="reactive")
-    pg.replay()
+    for _ in range(max(1, -(-warm // pg.steps))):
+        pg.replay()
     rem = K % pg.steps
     torch.cuda.synchronize()
 

@@ -34,12 +34,21 @@ namespace ffmp_detail {
 int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_error())
 // ffmp_conv2d_check: run every shape check of a launch, then return before launching
 thread_local bool t_conv_dry = false;
-// the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 16 = 16x16x32
-// (default), 32 = 32x32x16
-int g_conv_mfma = 16;
+// the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 0 = each kernel's
+// measured best (profiles/r06a_conv_ab.txt: 16x16x32 for the samples-as-M data gradient, 32x32x16 for
+// the others), 16 = 16x16x32, 32 = 32x32x16
+int g_conv_mfma = 0;
+int mfma_for(int dflt) { return g_conv_mfma ? g_conv_mfma : dflt; }
 int conv_mfma_swap(int v) {
   const int prev = g_conv_mfma;
   g_conv_mfma = v;
+  return prev;
+}
+// kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = by shape, 1, 2 or 4
+int g_conv_kys = 0;
+int conv_kys_swap(int v) {
+  const int prev = g_conv_kys;
+  g_conv_kys = v;
   return prev;
 }
 }
@@ -191,7 +200,7 @@ __device__ __forceinline__ bf16x8 load_bfrag_ms(const __bf16* __restrict__ w, in
   }
 }
 
-template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32>
+template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32, int KYS = 1>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
@@ -235,8 +244,8 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
     const int real = yr - pad;
     return (real >= 0 && real < H) ? xb + (size_t)real * gin.y : nullptr;
   };
-  // ring rows for the first kernel row
-  for (int row = yf + ky_lo; row <= yl + ky_lo; ++row) {
+  // ring rows for the first chunk of kernel rows
+  for (int row = yf + ky_lo; row <= yl + min(ky_lo + KYS - 1, ky_hi); ++row) {
     uint4 buf[4];
     load_row_regs<C>(row_src(row), chunks, gin.x, buf);
     store_row_lds<C>(lds + (row % RING) * pitch, chunks, buf);
@@ -268,66 +277,83 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   bf16x8 bnx[AN][KSTEPS];  // kBAhead 2: the ping-pong partner of bcur
   load_b(min(wk_lo, KH - 1) * KW, bcur);
 
-  for (int ky = ky_lo; ky <= ky_hi; ++ky) {
-    uint4 nrow[4];
-    const bool more = ky < ky_hi;
-    if (more) load_row_regs<C>(row_src(yl + ky + 1), chunks, gin.x, nrow);
-    if (ky >= wk_lo && ky <= wk_hi) {
-      int aoff[AM];
+  // kernel rows in chunks of KYS per ring step: the chunk's rows are in the ring, the next chunk's
+  // KYS rows are loaded into registers during it and written after it (KYS = 1: before the chunk's
+  // barrier, into the ring's spare slot; KYS > 1: between two barriers, over the rows the chunk was
+  // the last to read — ring = span + KYS - 1 slots, one barrier pair per KYS kernel rows)
+  for (int ky0 = ky_lo; ky0 <= ky_hi; ky0 += KYS) {
+    const int kyn = min(KYS, ky_hi - ky0 + 1);
+    const int nnext = min(KYS, ky_hi - (ky0 + kyn) + 1);  // rows of the next chunk (<= 0: none)
+    uint4 nrow[KYS][4];
 #pragma unroll
-      for (int mb = 0; mb < AM; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
-      // the MFMAs of tap (ky, kx) with its B fragments
-      auto tap = [&](int kx, const bf16x8 (&bt)[AN][KSTEPS]) {
-        // the lane's column of each block, or the zero column outside the tensor (PAD)
-        int abase[AM];
+    for (int j = 0; j < KYS; ++j)
+      if (j < nnext) load_row_regs<C>(row_src(yl + ky0 + kyn + j), chunks, gin.x, nrow[j]);
+    for (int ky = ky0; ky < ky0 + kyn; ++ky) {
+      if (ky >= wk_lo && ky <= wk_hi) {
+        int aoff[AM];
 #pragma unroll
-        for (int mb = 0; mb < AM; ++mb) {
-          const int col = xcol[mb] + kx * dx;
-          abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + kh * 16;
-        }
+        for (int mb = 0; mb < AM; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
+        // the MFMAs of tap (ky, kx) with its B fragments
+        auto tap = [&](int kx, const bf16x8 (&bt)[AN][KSTEPS]) {
+          // the lane's column of each block, or the zero column outside the tensor (PAD)
+          int abase[AM];
 #pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-          bf16x8 a[AM];
+          for (int mb = 0; mb < AM; ++mb) {
+            const int col = xcol[mb] + kx * dx;
+            abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + kh * 16;
+          }
 #pragma unroll
-          for (int mb = 0; mb < AM; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
+          for (int s = 0; s < KSTEPS; ++s) {
+            bf16x8 a[AM];
 #pragma unroll
-          for (int mb = 0; mb < AM; ++mb)
+            for (int mb = 0; mb < AM; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
 #pragma unroll
-            for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[mb], bt[nb][s], acc[mb][nb]);
-        }
-      };
-      if constexpr (kBAhead == 2) {
-        // two taps per trip, B in two register sets that swap roles without copies: the next tap's
-        // fragments are requested before this tap's MFMAs and waited for a whole tap later
-        int kx = 0;
-        for (; kx + 1 < KW; kx += 2) {
-          load_b(ky * KW + kx + 1, bnx);
-          tap(kx, bcur);
-          load_b(ky * KW + kx + 2, bcur);
-          tap(kx + 1, bnx);
-        }
-        if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
-          load_b(ky * KW + kx + 1, bnx);
-          tap(kx, bcur);
+            for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-          for (int nb = 0; nb < AN; ++nb)
+              for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[mb], bt[nb][s], acc[mb][nb]);
+          }
+        };
+        if constexpr (kBAhead == 2) {
+          // two taps per trip, B in two register sets that swap roles without copies: the next tap's
+          // fragments are requested before this tap's MFMAs and waited for a whole tap later
+          int kx = 0;
+          for (; kx + 1 < KW; kx += 2) {
+            load_b(ky * KW + kx + 1, bnx);
+            tap(kx, bcur);
+            load_b(ky * KW + kx + 2, bcur);
+            tap(kx + 1, bnx);
+          }
+          if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
+            load_b(ky * KW + kx + 1, bnx);
+            tap(kx, bcur);
 #pragma unroll
-            for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnx[nb][s];
-        }
-      } else {
-        for (int kx = 0; kx < KW; ++kx) {
-          bf16x8 bnext[AN][KSTEPS];
-          load_b(ky * KW + kx + 1, bnext);
-          tap(kx, bcur);
+            for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
-          for (int nb = 0; nb < AN; ++nb)
+              for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnx[nb][s];
+          }
+        } else {
+          for (int kx = 0; kx < KW; ++kx) {
+            bf16x8 bnext[AN][KSTEPS];
+            load_b(ky * KW + kx + 1, bnext);
+            tap(kx, bcur);
 #pragma unroll
-            for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnext[nb][s];
+            for (int nb = 0; nb < AN; ++nb)
+#pragma unroll
+              for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnext[nb][s];
+          }
         }
       }
     }
-    if (more) store_row_lds<C>(lds + ((yl + ky + 1) % RING) * pitch, chunks, nrow);
-    __syncthreads();
+    if constexpr (KYS == 1) {
+      if (nnext > 0) store_row_lds<C>(lds + ((yl + ky0 + 1) % RING) * pitch, chunks, nrow[0]);
+      __syncthreads();
+    } else {
+      __syncthreads();  // every wave done with the rows the new ones replace
+#pragma unroll
+      for (int j = 0; j < KYS; ++j)
+        if (j < nnext) store_row_lds<C>(lds + ((yl + ky0 + kyn + j) % RING) * pitch, chunks, nrow[j]);
+      __syncthreads();
+    }
   }
 
   // epilogue: C/D column = lane & (MS - 1) (channel), row = Mfma<MS>::row(i, kh) (position)
@@ -495,7 +521,7 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
   const dim3 grid((Ho * Wo + 127) / 128, B);
   if (t_conv_dry) return FFMP_OK;
-  if (ffmp_detail::g_conv_mfma == 16)
+  if (ffmp_detail::mfma_for(32) == 16)
     hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
                        (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, flags);
   else
@@ -537,19 +563,40 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   const int Ho = H + 2 * pad - KH + 1, Wo = W + 2 * pad - (KW - 1) * dx;
   constexpr int PT = kWaves * MBW * 32;
   const int span = (PT + Wo - 1) / Wo + 1;  // input rows a tile reads for one ky
-  const int ring = span + 1;                // + the row loaded for the next ky
-  const size_t lds = (size_t)ring * lds_pitch<C>(W) + C * 2;  // + the zero column
+  const size_t pitch = (size_t)lds_pitch<C>(W);
+  // kernel rows per ring step (FFMP_TUNE_CONV_KYS; 0 = auto): the one-channel-block kernels (the folded
+  // conv1, the padded data gradient) carry few MFMAs per kernel row, so their per-row barrier and row
+  // latency show (conv1: parked 0.43 of its wave cycles, profiles/r05e_conv_pmc.txt): 4 rows per step
+  // where the ring (span + 3 slots) leaves two workgroups per CU, else 2, else 1
+  auto ring_of = [&](int k) { return k == 1 ? span + 1 : span + k - 1; };
+  auto lds_of = [&](int k) { return (size_t)ring_of(k) * pitch + C * 2; };  // + the zero column
+  int kys = ffmp_detail::g_conv_kys;
+  if (kys == 0) kys = (NB == 1 && lds_of(4) <= 80 * 1024) ? 4 : (NB == 1 && lds_of(2) <= 80 * 1024) ? 2 : 1;
+  if (kys != 1 && kys != 2 && kys != 4) kys = 1;
+  const int ring = ring_of(kys);
+  const size_t lds = lds_of(kys);
   if (lds > 160 * 1024)
     return fail(FFMP_E_ARG, "ffmp_conv2d: a ring of %d input rows (%zu bytes) exceeds the 160 KiB LDS", ring, lds);
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
   if (t_conv_dry) return FFMP_OK;
-  if (ffmp_detail::g_conv_mfma == 16)
-    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
+  auto go = [&](auto MS_, auto KYS_) {
+    constexpr int kMS = decltype(MS_)::value, kKYS = decltype(KYS_)::value;
+    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, kMS, kKYS>), grid, dim3(256), lds, s, (const __bf16*)x,
                        (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32>), grid, dim3(256), lds, s, (const __bf16*)x,
-                       (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+  };
+  auto with_ms = [&](auto KYS_) {
+    if (ffmp_detail::mfma_for(32) == 16) go(std::integral_constant<int, 16>{}, KYS_);
+    else go(std::integral_constant<int, 32>{}, KYS_);
+  };
+  if constexpr (NB == 1) {
+    if (kys == 4) with_ms(std::integral_constant<int, 4>{});
+    else if (kys == 2) with_ms(std::integral_constant<int, 2>{});
+    else with_ms(std::integral_constant<int, 1>{});
+  } else {
+    if (kys == 2) with_ms(std::integral_constant<int, 2>{});
+    else with_ms(std::integral_constant<int, 1>{});
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
   return FFMP_OK;
@@ -822,7 +869,7 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   const int TKX = std::min(KW, TG), TKY = TG / TKX;
   if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
   // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
-  const int ms = ffmp_detail::g_conv_mfma == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
+  const int ms = ffmp_detail::mfma_for(32) == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
   int R = std::min(Ho, 8);
   auto bytes = [&](int rr) { return (size_t)(rr * Wo + kp) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
   auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };
@@ -1025,7 +1072,7 @@ int launch_dgrad_bm(const void* g, const void* w, void* y, int B, int Hy, int Wy
   const long blocks = (long)Hx * ((B + 31) / 32);
   if (blocks > 0x7fffffffL) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: grid too large");
   if (t_conv_dry) return FFMP_OK;
-  if (ffmp_detail::g_conv_mfma == 16)
+  if (ffmp_detail::mfma_for(16) == 16)
     hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ, 16>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
                        (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
   else

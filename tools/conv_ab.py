@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""A/B of the convolution kernels' MFMA shape (FFMP_TUNE_CONV_MFMA: 16 = 16x16x32, 32 = 32x32x16) on
-the reference Network's layers at batch B (default 256), random data, interleaved rounds in ONE process
-(cdna_hip_programming.md rule 24): per layer and shape the median / min ms and PF/s over the rounds,
-and each shape's max error against a float64 convolution of the same bf16 operands (first 4 samples).
-Usage: python tools/conv_ab.py [B] [rounds]"""
+"""A/B of the convolution kernels' launch variants — the MFMA shape (FFMP_TUNE_CONV_MFMA: 16 = 16x16x32,
+32 = 32x32x16) and the kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS: 0 = by shape,
+1, 2, 4) — on the reference Network's layers at batch B (default 256), random data, interleaved rounds in
+ONE process (cdna_hip_programming.md rule 24): per layer and variant the median / min ms and PF/s over
+the rounds, and each variant's max error against a float64 convolution of the same bf16 operands (first
+4 samples).  Usage: python tools/conv_ab.py [B] [rounds] [variant ...]   (variant = mfma:kys, e.g. 32:1)"""
 import os
 import sys
 
@@ -19,7 +20,7 @@ from flow_field_based_motion_planner_amd.conv_mfma import (conv2d_dgrad_nhwc, co
 dev = torch.device("cuda:0")
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-SHAPES = (16, 32)
+VARIANTS = [tuple(int(v) for v in a.split(":")) for a in sys.argv[3:]] or [(0, 0), (32, 1), (32, 2), (32, 4), (16, 4), (16, 0)]
 torch.manual_seed(0)
 
 
@@ -72,10 +73,15 @@ layers["conv3 fwd (small)"] = (2.0 * B * 31 * 31 * 64 * 64 * 64, lambda: conv2d_
                                lambda: F.relu(F.conv2d(x3[:4].permute(0, 3, 1, 2).double(), w3.double(), b3.double())))
 
 lib = _abi.load()
-res = {k: {s: [] for s in SHAPES} for k in layers}
+def setv(v):
+    lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, v[0])
+    lib.ffmp_set_tuning(_abi.TUNE_CONV_KYS, v[1])
+
+
+res = {k: {s: [] for s in VARIANTS} for k in layers}
 errs = {k: {} for k in layers}
-for s in SHAPES:  # correctness per shape (and warm-up)
-    lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, s)
+for s in VARIANTS:  # correctness per variant (and warm-up)
+    setv(s)
     for k, (flop, fn, ref) in layers.items():
         out = fn()
         torch.cuda.synchronize()
@@ -86,15 +92,15 @@ for s in SHAPES:  # correctness per shape (and warm-up)
                 o = o.permute(0, 3, 1, 2)
             errs[k][s] = float((o - r).abs().max() / (r.abs().max() + 1e-9))
 for rnd_i in range(ROUNDS):
-    for s in SHAPES:
-        lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, s)
+    for s in VARIANTS:
+        setv(s)
         for k, (flop, fn, ref) in layers.items():
             res[k][s].append(timeit(fn))
-lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, 16)
+setv((0, 0))
 for k, (flop, fn, ref) in layers.items():
     line = [f"{k:20s} B={B}"]
-    for s in SHAPES:
+    for s in VARIANTS:
         v = sorted(res[k][s])
         med = v[len(v) // 2]
-        line.append(f"mfma{s}: med {med:.4f} ms min {v[0]:.4f} ({flop / med / 1e12:.3f} PF/s) err {errs[k].get(s, float('nan')):.2e}")
+        line.append(f"{s[0]}:{s[1]}: med {med:.4f} ms min {v[0]:.4f} ({flop / med / 1e12:.3f} PF/s) err {errs[k].get(s, float('nan')):.2e}")
     print(" | ".join(line), flush=True)

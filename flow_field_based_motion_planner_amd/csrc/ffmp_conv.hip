@@ -44,6 +44,13 @@ int conv_mfma_swap(int v) {
   g_conv_mfma = v;
   return prev;
 }
+// the row-ring forward's B operand through LDS (FFMP_TUNE_CONV_LB): 0 = off (default), 1 = on where it fits
+int g_conv_lb = 0;
+int conv_lb_swap(int v) {
+  const int prev = g_conv_lb;
+  g_conv_lb = v;
+  return prev;
+}
 // kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = by shape, 1, 2 or 4
 int g_conv_kys = 0;
 int conv_kys_swap(int v) {
@@ -381,6 +388,138 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   }
 }
 
+// The row-ring forward with each tap's B operand shared through LDS (FFMP_TUNE_CONV_LB): the
+// workgroup's 256 threads load the next tap's weights (N x C x 2 bytes = 4 KiB at conv2's shape, one
+// 16-byte chunk per thread) into registers during the current tap and write them, in fragment order,
+// into the other of two LDS tap buffers; one barrier per tap publishes them, and every wave reads its
+// B fragments from LDS (1 KiB contiguous per fragment: conflict-free ds_read_b128) instead of from
+// L1/L2 — a quarter of the weight requests, 4 staging registers instead of a 16-register next-tap
+// set.  The ring holds exactly the tile's span of rows (no spare slot): the next row is written
+// between two barriers at the end of each kernel row.  Unpadded (pad 0), plain or fragment-order
+// weights, C * N * 2 == 4096 bytes per tap (256 chunks).
+template <int C, int NB, int MBW, bool WF>
+__global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_lb_kernel(const __bf16* __restrict__ x,
+                                                                             const __bf16* __restrict__ w,
+                                                                             const float* __restrict__ bias,
+                                                                             void* __restrict__ y, int H, int W, int KH,
+                                                                             int KW, int dx, int RING, int flags) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int N = NB * 32;
+  constexpr int PT = kWaves * MBW * 32;
+  constexpr int TAPB = N * C * 2;  // bytes of one tap's weights
+  static_assert(TAPB == 4096, "one 16-byte chunk per thread per tap");
+  const int Ho = H - KH + 1, Wo = W - (KW - 1) * dx;
+  const int b = blockIdx.y;
+  const int P = Ho * Wo;
+  const int p0 = blockIdx.x * PT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int rowbytes = W * C * 2;
+  const int pitch = lds_pitch<C>(W);
+  const int chunks = rowbytes / 16;
+  const int2 gin = in_geom<C>(W, dx, flags);
+  char* bbuf = lds + RING * pitch;  // two tap buffers after the ring
+  const int yf = p0 / Wo;
+  const int yl = min(P - 1, p0 + PT - 1) / Wo;
+  const char* xb = (const char*)x + (size_t)b * H * gin.y;
+  const int pw0 = p0 + wave * MBW * 32;
+  int ypos[MBW], xcol[MBW];
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb) {
+    const int m = min(pw0 + mb * 32 + r, P - 1);
+    ypos[mb] = m / Wo;
+    xcol[mb] = m - ypos[mb] * Wo;
+  }
+  // this thread's chunk of a tap: global chunk q = threadIdx.x -> its fragment-order LDS offset
+  const int q = threadIdx.x;
+  int bdst;
+  if constexpr (WF) {
+    bdst = q * 16;
+  } else {  // plain [n][c]: n = q / (C / 8), 8 channels c0 = (q % (C / 8)) * 8
+    const int n = q / (C / 8), c0 = (q % (C / 8)) * 8;
+    bdst = ((((n >> 5) * (C / 16) + (c0 >> 4)) * 2 + ((c0 >> 3) & 1)) * 256 + (n & 31) * 8) * 2;
+  }
+  const char* wsrc = (const char*)w + q * 16;
+  for (int row = yf; row <= yl; ++row) {
+    uint4 buf[4];
+    load_row_regs<C>(xb + (size_t)row * gin.y, chunks, gin.x, buf);
+    store_row_lds<C>(lds + (row % RING) * pitch, chunks, buf);
+  }
+  *(uint4*)(bbuf + bdst) = *(const uint4*)wsrc;  // tap 0 into buffer 0
+  __syncthreads();
+
+  f32x16 acc[MBW][NB];
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x16{};
+  const int ntaps = KH * KW;
+  int t = 0;
+  for (int ky = 0; ky < KH; ++ky) {
+    uint4 nrow[4];
+    const bool more = ky + 1 < KH;
+    if (more) load_row_regs<C>(xb + (size_t)(yl + ky + 1) * gin.y, chunks, gin.x, nrow);
+    int aoff[MBW];
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
+    for (int kx = 0; kx < KW; ++kx, ++t) {
+      const bool bnext = t + 1 < ntaps;
+      uint4 stage = uint4{0u, 0u, 0u, 0u};
+      if (bnext) stage = *(const uint4*)(wsrc + (size_t)(t + 1) * TAPB);
+      const char* bt = bbuf + (t & 1) * TAPB;
+      bf16x8 bf[NB][C / 16];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int s2 = 0; s2 < C / 16; ++s2)
+          bf[nb][s2] = *(const bf16x8*)(bt + (((nb * (C / 16) + s2) * 2 + h) * 256 + r * 8) * 2);
+      int abase[MBW];
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) abase[mb] = aoff[mb] + cell_off<C>(xcol[mb] + kx * dx) + h * 16;
+#pragma unroll
+      for (int s2 = 0; s2 < C / 16; ++s2) {
+        bf16x8 a[MBW];
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s2 * 32);
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], bf[nb][s2], acc[mb][nb], 0, 0, 0);
+      }
+      if (bnext) *(uint4*)(bbuf + ((t + 1) & 1) * TAPB + bdst) = stage;
+      __syncthreads();  // tap t + 1's weights published; tap t's buffer free again
+    }
+    if (more) {  // the slot of row yf + ky (no wave reads it any more) takes row yl + ky + 1
+      store_row_lds<C>(lds + ((yl + ky + 1) % RING) * pitch, chunks, nrow);
+      __syncthreads();
+    }
+  }
+
+  const bool relu = flags & FFMP_CONV_RELU, out_bf16 = flags & FFMP_CONV_OUT_BF16;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int n = nb * 32 + r;
+    const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) {
+      const int mbase = pw0 + mb * 32;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = mbase + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m >= P) continue;
+        float v = acc[mb][nb][i] + bn;
+        if (relu) v = fmaxf(v, 0.f);
+        const size_t o = ((size_t)b * P + m) * N + n;
+        if (out_bf16)
+          ((__bf16*)y)[o] = (__bf16)v;
+        else
+          ((float*)y)[o] = v;
+      }
+    }
+  }
+}
+
 // Small images (the reference Network's conv3 / conv4: 8 x 8 kernels over 38^2 .. 17^2 maps, and
 // their data gradients): a 512-position tile wastes most of its positions on a 10^2 or 17^2
 // image, and 128-position tiles leave each wave one 32-position block (every B fragment used
@@ -579,6 +718,18 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
     return fail(FFMP_E_ARG, "ffmp_conv2d: a ring of %d input rows (%zu bytes) exceeds the 160 KiB LDS", ring, lds);
   if ((W * C * 2) / 16 > 4 * 256) return fail(FFMP_E_ARG, "ffmp_conv2d: input rows wider than 16 KiB");
   const dim3 grid((Ho * Wo + PT - 1) / PT, B);
+  // B through LDS (FFMP_TUNE_CONV_LB): the unpadded 4 KiB-per-tap layers, ring = span + two tap buffers
+  if constexpr (C * NB * 32 * 2 == 4096) {
+    const size_t lds_lb = (size_t)span * pitch + 2 * 4096;
+    if (!PAD && ffmp_detail::g_conv_lb == 1 && lds_lb <= 80 * 1024) {
+      if (t_conv_dry) return FFMP_OK;
+      hipLaunchKernelGGL((conv_fwd_lb_kernel<C, NB, MBW, WF>), grid, dim3(256), lds_lb, s, (const __bf16*)x,
+                         (const __bf16*)w, bias, y, H, W, KH, KW, dx, span, flags);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d launch: %s", hipGetErrorString(e));
+      return FFMP_OK;
+    }
+  }
   if (t_conv_dry) return FFMP_OK;
   auto go = [&](auto MS_, auto KYS_) {
     constexpr int kMS = decltype(MS_)::value, kKYS = decltype(KYS_)::value;

@@ -44,6 +44,7 @@ __attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
 int32_t ring_extra_swap(int32_t v);  // ffmp_ring.hip (FFMP_TUNE_RING_EXTRA)
 int conv_mfma_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_MFMA)
 int conv_kys_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_KYS)
+int conv_lb_swap(int v);             // ffmp_conv.hip (FFMP_TUNE_CONV_LB)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1731,6 +1732,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       if (value != 0 && value != 1 && value != 2 && value != 4)
         return fail(FFMP_E_ARG, "conv kernel rows per ring step must be 0 (by shape), 1, 2 or 4");
       return ffmp_detail::conv_kys_swap(value);
+    case FFMP_TUNE_CONV_LB:
+      if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv B-through-LDS must be 0 or 1");
+      return ffmp_detail::conv_lb_swap(value);
     case FFMP_TUNE_RING_EXTRA:
       if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");
       return ffmp_detail::ring_extra_swap(value);

@@ -195,6 +195,8 @@ int64_t ffmp_layout(int32_t which);
                                    (v_mfma_f32_32x32x16_bf16); the same products, fp32 sums in another order */
 #define FFMP_TUNE_CONV_KYS 8    /* kernel rows per ring step of the row-ring convolution forward: 0 (default,
                                    by shape), 1, 2 or 4 (the same products and sums) */
+#define FFMP_TUNE_CONV_LB 9     /* 1: the unpadded row-ring forward shares each tap's weights through LDS
+                                   (one barrier per tap); 0 (default): from L1/L2 per wave */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

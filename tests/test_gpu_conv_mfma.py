@@ -251,3 +251,77 @@ def test_conv_x_fold_equals_materialized_fold(Cc, wide):
         ref = conv2d_nhwc(fold_input(x, F), wk, bias, relu=True, out_dtype=torch.bfloat16, dx=F)
         got = conv2d_nhwc(xn, wk, bias, relu=True, out_dtype=torch.bfloat16, dx=F, x_fold=True)
         assert got.shape == ref.shape and torch.equal(got, ref)
+
+
+@pytest.fixture
+def conv_knobs():
+    from flow_field_based_motion_planner_amd import _abi
+    lib = _abi.load()
+
+    def setk(mfma=0, kys=0, lb=0):
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, mfma)
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_KYS, kys)
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_LB, lb)
+    yield setk
+    setk()
+
+
+@pytest.mark.parametrize("B,H,W,C,K,N,pad,dx", [
+    (2, 69, 69, 32, 32, 64, 0, 1),    # conv2 (row-ring; LB route)
+    (2, 38, 38, 64, 32, 32, 31, 1),   # the padded data-gradient form (one channel block: KYS 4)
+    (2, 100, 85, 32, 32, 32, 0, 16),  # conv1 folded (one channel block, dx = 16)
+    (3, 38, 38, 64, 8, 64, 0, 1),     # conv3 (small-image kernel)
+    (2, 12, 12, 64, 2, 64, 1, 1), (5, 33, 70, 32, 2, 64, 0, 1), (2, 40, 45, 32, 5, 32, 0, 1)])
+def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, dx):
+    """Every launch variant of the forward (FFMP_TUNE_CONV_MFMA 16 / 32, FFMP_TUNE_CONV_KYS 1 / 2 / 4,
+    FFMP_TUNE_CONV_LB) against float64 within the forward's tolerance; the variants that keep the
+    32x32x16 accumulation order (kernel rows per ring step, B through LDS) bit-identical to the default."""
+    g = torch.Generator(device=DEV).manual_seed(B + H + K + pad)
+    xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)
+    KW = 2 if dx > 1 else K
+    w = torch.randn((N, C, K, KW), device=DEV, generator=g) / (C * K * KW) ** 0.5
+    bias = torch.randn(N, device=DEV, generator=g) * 0.1
+    wp = pack_weight(w)
+    x64 = xb.double().permute(0, 3, 1, 2)
+    w64 = wp.double().permute(2, 3, 0, 1)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = F.conv2d(x64, w64, bias.double(), padding=pad, dilation=(1, dx)).permute(0, 2, 3, 1)
+        absref = F.conv2d(x64.abs(), w64.abs(), padding=pad, dilation=(1, dx)).permute(0, 2, 3, 1)
+    conv_knobs(32, 1, 0)
+    base = conv2d_nhwc(xb, wp, bias, pad=pad, dx=dx)
+    for mfma, kys, lb in [(32, 1, 0), (32, 2, 0), (32, 4, 0), (32, 1, 1), (16, 1, 0), (16, 4, 0), (0, 0, 0)]:
+        conv_knobs(mfma, kys, lb)
+        for wk in (wp, frag_order(wp)):
+            y = conv2d_nhwc(xb, wk, bias, pad=pad, dx=dx)
+            err = (y.double() - ref).abs()
+            bad = err > 5e-5 * absref + 1e-6
+            assert not bool(bad.any()), (mfma, kys, lb, int(bad.sum()), float(err.max()))
+            if mfma in (0, 32):  # the default forward keeps 32x32x16
+                assert torch.equal(y, base), (mfma, kys, lb)
+
+
+@pytest.mark.parametrize("mfma", [16, 32])
+def test_dgrad_and_wgrad_mfma_shapes_match_float64(conv_knobs, mfma):
+    """The samples-as-M data gradient and the weight gradient on both MFMA shapes (conv2's shapes at a
+    small batch, and the folded conv1's weight gradient) against float64."""
+    from flow_field_based_motion_planner_amd.conv_mfma import conv2d_dgrad_nhwc, conv2d_wgrad_nhwc, pack_weight_dgrad_bm
+    conv_knobs(mfma, 0, 0)
+    g0 = torch.Generator(device=DEV).manual_seed(mfma)
+    g = torch.randn((33, 38, 38, 64), device=DEV, generator=g0).to(torch.bfloat16)
+    w = torch.randn((64, 32, 32, 32), device=DEV, generator=g0) / 181.0
+    dx = conv2d_dgrad_nhwc(g, pack_weight_dgrad_bm(w), out_dtype=torch.float32)
+    g64, w64 = g.double().permute(0, 3, 1, 2), w.to(torch.bfloat16).double()
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = torch.nn.grad.conv2d_input((33, 32, 69, 69), w64, g64).permute(0, 2, 3, 1)
+        absref = torch.nn.grad.conv2d_input((33, 32, 69, 69), w64.abs(), g64.abs()).permute(0, 2, 3, 1)
+    assert not bool(((dx.double() - ref).abs() > 5e-5 * absref + 1e-6).any())
+    for (B, H, W, C, KH, KW, N, d) in [(3, 69, 69, 32, 32, 32, 64, 1), (2, 100, 85, 32, 32, 2, 32, 16),
+                                       (2, 20, 22, 32, 6, 4, 32, 1)]:
+        x = torch.randn((B, H, W, C), device=DEV, generator=g0).to(torch.bfloat16)
+        gy = torch.randn((B, H - KH + 1, W - (KW - 1) * d, N), device=DEV, generator=g0).to(torch.bfloat16)
+        dw = conv2d_wgrad_nhwc(gy, x, KH, KW, dx=d)
+        x64, gy64 = x.double().permute(0, 3, 1, 2), gy.double().permute(0, 3, 1, 2)
+        with torch.backends.cudnn.flags(enabled=False):
+            rw = torch.nn.grad.conv2d_weight(x64, (N, C, KH, KW), gy64, dilation=(1, d)).permute(2, 3, 0, 1)
+            aw = torch.nn.grad.conv2d_weight(x64.abs(), (N, C, KH, KW), gy64.abs(), dilation=(1, d)).permute(2, 3, 0, 1)
+        assert not bool(((dw.double() - rw).abs() > 5e-5 * aw + 1e-6).any()), (mfma, B, H, KH)

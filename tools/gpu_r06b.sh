@@ -1,15 +1,17 @@
 #!/bin/bash
-# round 6 (b): conv variants A/B (MFMA shape x kernel rows per ring step), the 16x16x32 data gradient
-# default, re-warmed bench legs (C4 shard at the driver's 20 steps), closed-loop, legacy edges, HBM tests.
+# round 6 (b): conv launch variants (MFMA shape, kernel rows per ring step, B through LDS): parity + A/B;
+# legacy edges, closed loop, learner, HBM tests; re-warmed bench legs (C4 shard at the driver's 20 steps).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r06b
 mkdir -p $O
 cd $R
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
-timeout -k 10 300 python -u tools/conv_ab.py 256 7 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_conv_mfma.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_conv.log 2>&1; rc=$?
+tail -3 $O/pytest_conv.log; grep -E "^FAILED|Error" $O/pytest_conv.log | head -20; ok $rc || exit 1
+timeout -k 10 300 python -u tools/conv_ab.py 256 7 0:0:0 32:1:0 32:1:1 32:2:0 32:4:0 16:4:0 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
 cat $O/conv_ab.txt
-timeout -k 10 900 python -u -m pytest tests/test_gpu_conv_mfma.py tests/test_gpu_legacy_api.py tests/test_gpu_closed_loop.py tests/test_gpu_learner.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_legacy_api.py tests/test_gpu_closed_loop.py tests/test_gpu_learner.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; grep -E "^FAILED|Error" $O/pytest.log | head -20; ok $rc || exit 1
 timeout -k 10 900 python -u -m pytest tests/test_gpu_hbm_budget.py -m gpu -v -s --timeout 600 --timeout-method thread > $O/pytest_hbm.log 2>&1; rc=$?
 tail -15 $O/pytest_hbm.log; ok $rc || exit 1

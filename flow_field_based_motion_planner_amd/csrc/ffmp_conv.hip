@@ -35,8 +35,9 @@ int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_e
 // ffmp_conv2d_check: run every shape check of a launch, then return before launching
 thread_local bool t_conv_dry = false;
 // the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 0 = each kernel's
-// measured best (profiles/r06a_conv_ab.txt: 16x16x32 for the samples-as-M data gradient, 32x32x16 for
-// the others), 16 = 16x16x32, 32 = 32x32x16
+// default (32x32x16 everywhere: profiles/r06a_conv_ab.txt, r06b_conv_ab.txt — the 16x16x32 stream ran
+// 6-50 % slower on the forwards and the weight gradient, and the samples-as-M data gradient within
+// the run-to-run spread of 32x32x16), 16 = 16x16x32, 32 = 32x32x16
 int g_conv_mfma = 0;
 int mfma_for(int dflt) { return g_conv_mfma ? g_conv_mfma : dflt; }
 int conv_mfma_swap(int v) {
@@ -45,13 +46,15 @@ int conv_mfma_swap(int v) {
   return prev;
 }
 // the row-ring forward's B operand through LDS (FFMP_TUNE_CONV_LB): 0 = off (default), 1 = on where it fits
+// (conv2's forward 1.35 against 1.28 ms: the per-tap barrier costs more than the shared weight loads
+// save, profiles/r06b_conv_ab.txt)
 int g_conv_lb = 0;
 int conv_lb_swap(int v) {
   const int prev = g_conv_lb;
   g_conv_lb = v;
   return prev;
 }
-// kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = by shape, 1, 2 or 4
+// kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = default (1), 1, 2 or 4
 int g_conv_kys = 0;
 int conv_kys_swap(int v) {
   const int prev = g_conv_kys;
@@ -703,14 +706,14 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   constexpr int PT = kWaves * MBW * 32;
   const int span = (PT + Wo - 1) / Wo + 1;  // input rows a tile reads for one ky
   const size_t pitch = (size_t)lds_pitch<C>(W);
-  // kernel rows per ring step (FFMP_TUNE_CONV_KYS; 0 = auto): the one-channel-block kernels (the folded
-  // conv1, the padded data gradient) carry few MFMAs per kernel row, so their per-row barrier and row
-  // latency show (conv1: parked 0.43 of its wave cycles, profiles/r05e_conv_pmc.txt): 4 rows per step
-  // where the ring (span + 3 slots) leaves two workgroups per CU, else 2, else 1
+  // kernel rows per ring step (FFMP_TUNE_CONV_KYS; 0 = default 1).  Built for the one-channel-block
+  // layers (conv1 carries 16 MFMAs per wave per kernel row and parks 0.43 of its wave cycles,
+  // profiles/r05e_conv_pmc.txt) but measured slower: conv1 0.269 ms at 1 row per step, 0.296 at 2 and
+  // 4; conv2 1.28 / 1.27 / 1.51 ms (profiles/r06b_conv_ab.txt) — kept as a probe knob, default 1
   auto ring_of = [&](int k) { return k == 1 ? span + 1 : span + k - 1; };
   auto lds_of = [&](int k) { return (size_t)ring_of(k) * pitch + C * 2; };  // + the zero column
   int kys = ffmp_detail::g_conv_kys;
-  if (kys == 0) kys = (NB == 1 && lds_of(4) <= 80 * 1024) ? 4 : (NB == 1 && lds_of(2) <= 80 * 1024) ? 2 : 1;
+  if (kys == 0) kys = 1;
   if (kys != 1 && kys != 2 && kys != 4) kys = 1;
   const int ring = ring_of(kys);
   const size_t lds = lds_of(kys);
@@ -1223,7 +1226,7 @@ int launch_dgrad_bm(const void* g, const void* w, void* y, int B, int Hy, int Wy
   const long blocks = (long)Hx * ((B + 31) / 32);
   if (blocks > 0x7fffffffL) return fail(FFMP_E_ARG, "ffmp_conv2d_dgrad: grid too large");
   if (t_conv_dry) return FFMP_OK;
-  if (ffmp_detail::mfma_for(16) == 16)
+  if (ffmp_detail::mfma_for(32) == 16)
     hipLaunchKernelGGL((conv_dgrad_bm_kernel<C, N, NW, PW, KQ, 16>), dim3((unsigned)blocks), dim3(NW * 64), lds, s,
                        (const __bf16*)g, (const __bf16*)w, y, B, Hy, Wy, KH, KW, flags);
   else

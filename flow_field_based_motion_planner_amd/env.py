@@ -125,7 +125,7 @@ class FFMP(GymEnvBase):
         hit = self._cfg_cache.get(key)
         if hit is not None and hit[3] is self.cfg:  # (a config is replaced, never mutated: FFMPConfig.replace)
             self.robot_grids = hit[1]
-            return hit[0], hit[2]
+            return hit[0], hit[2]  # (ctypes cfg, complete)
         cells = []
         half = 0.5 * self.map_range
         for i in range(self.map_grid_num):
@@ -153,7 +153,7 @@ class FFMP(GymEnvBase):
         if len(self._cfg_cache) >= 64:
             self._cfg_cache.clear()
         complete = k_oor == len(cells)
-        self._cfg_cache[key] = ((c, complete), self.robot_grids, complete, self.cfg)
+        self._cfg_cache[key] = (c, self.robot_grids, complete, self.cfg)
         return c, complete
 
     @staticmethod

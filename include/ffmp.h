@@ -190,11 +190,11 @@ int64_t ffmp_layout(int32_t which);
                                    ones the ring needs (pairing candidates; they stay pooled):
                                    0 = default (need/2 + 4), v >= 1 = at most v - 1.  An HBM
                                    budget (FFMPVec hbm_budget) sets it around its ring creation. */
-#define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 0 (default: each
-                                   kernel's measured best), 16 (v_mfma_f32_16x16x32_bf16) or 32
+#define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 0 (default:
+                                   32x32x16, measured fastest), 16 (v_mfma_f32_16x16x32_bf16) or 32
                                    (v_mfma_f32_32x32x16_bf16); the same products, fp32 sums in another order */
 #define FFMP_TUNE_CONV_KYS 8    /* kernel rows per ring step of the row-ring convolution forward: 0 (default,
-                                   by shape), 1, 2 or 4 (the same products and sums) */
+                                   1), 1, 2 or 4 (the same products and sums) */
 #define FFMP_TUNE_CONV_LB 9     /* 1: the unpadded row-ring forward shares each tap's weights through LDS
                                    (one barrier per tap); 0 (default): from L1/L2 per wave */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);

@@ -54,6 +54,13 @@ int conv_lb_swap(int v) {
   g_conv_lb = v;
   return prev;
 }
+// the weight gradient's operand reads one k-step ahead (FFMP_TUNE_CONV_WGPF): 0 = by FFMP_WGRAD_PREFETCH, 1 = on
+int g_conv_wgpf = 0;
+int conv_wgpf_swap(int v) {
+  const int prev = g_conv_wgpf;
+  g_conv_wgpf = v;
+  return prev;
+}
 // kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = default (1), 1, 2 or 4
 int g_conv_kys = 0;
 int conv_kys_swap(int v) {
@@ -846,7 +853,7 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
 #ifndef FFMP_WGRAD_PREFETCH
 #define FFMP_WGRAD_PREFETCH 0
 #endif
-template <int C, int N, int TW, int MS = 32>
+template <int C, int N, int TW, int MS = 32, bool PF = false>
 __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
                                                             float* __restrict__ part, int B, int H, int W, int KH,
                                                             int KW, int dx, int TKY, int TKX, int R, int per_chunk) {
@@ -858,7 +865,9 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
   const int groups_x = KW / TKX;
   const int kyA = (blockIdx.x / groups_x) * TKY, kxA = (blockIdx.x % groups_x) * TKX;
   const int b0 = blockIdx.y * per_chunk, b1 = min(B, b0 + per_chunk);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave-uniform in a scalar register: the taps' offsets below are then scalar too (the compiler kept
+  // them in 16 VGPRs and spent two VALU per operand read on them, profiles/r06c_wgrad_isa.txt)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int fr = lane & (MS - 1), fk = lane / MS;       // operand row / k-chunk of 8 positions
   const int q = (lane & 15) >> 2, pp = lane & 3;        // tr-read: row q of 4, columns 4pp .. of 16
   const int gh = MS == 32 ? (lane >> 4) & 1 : 0;        // 32x32x16: the 16-column half of the 32
@@ -869,12 +878,13 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
 
   // this wave's taps of the rectangle (the host makes the rectangle tile the kernel exactly);
   // the B image row of (position row pr, column pc) at tap t: (pr + dky[t]) * W + pc + dkx[t]
-  int dky[TW], dkx[TW];
+  int dky[TW], dkx[TW], toff[TW];
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     const int k = wave * TW + t;
     dky[t] = k / TKX;
     dkx[t] = (kxA + k % TKX) * dx;
+    toff[t] = (dky[t] * W + dkx[t]) * (C * 2);  // byte offset of tap t's x row (unswizzled images)
   }
   for (int i = threadIdx.x; i < grow * KP / 16; i += 256) *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
 
@@ -939,15 +949,22 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
           ar[nb][u] = tr_read(gimg + grw * grow + off);
         }
         const int base = in ? pr[u] * W + pc[u] : 0;
+        if constexpr (C == 64) {  // 128-byte rows: the chunk swizzle depends on each read's row
 #pragma unroll
-        for (int t = 0; t < TW; ++t) {
-          const int xrw = base + dky[t] * W + dkx[t];
+          for (int t = 0; t < TW; ++t) {
+            const int xrw = base + dky[t] * W + dkx[t];
 #pragma unroll
-          for (int cb = 0; cb < AC; ++cb) {
-            const int col = acol0 + cb * MS * 2;
-            const int off = C == 64 ? ((col & ~15) ^ swz128(xrw)) | (col & 15) : col;
-            br[t][cb][u] = tr_read(ximg + xrw * xrowb + off);
+            for (int cb = 0; cb < AC; ++cb) {
+              const int col = acol0 + cb * MS * 2;
+              br[t][cb][u] = tr_read(ximg + xrw * xrowb + (((col & ~15) ^ swz128(xrw)) | (col & 15)));
+            }
           }
+        } else {  // one lane address per k row, plus a scalar tap offset and a constant column offset
+          const char* xl = ximg + base * xrowb + acol0;
+#pragma unroll
+          for (int t = 0; t < TW; ++t)
+#pragma unroll
+            for (int cb = 0; cb < AC; ++cb) br[t][cb][u] = tr_read(xl + toff[t] + cb * MS * 2);
         }
         int c = pc[u] + KP, rr = pr[u];
 #pragma unroll
@@ -975,8 +992,8 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
 #pragma unroll
           for (int cb = 0; cb < AC; ++cb) acc[t][nb][cb] = M::mma(a[nb], bb[t][cb], acc[t][nb][cb]);
     };
-    constexpr bool kPrefetch = FFMP_WGRAD_PREFETCH < 0 ? TW * AN * AC * (MS / 16) * (MS / 16) >= 64
-                                                       : FFMP_WGRAD_PREFETCH != 0;
+    constexpr bool kPrefetch = PF || (FFMP_WGRAD_PREFETCH < 0 ? TW * AN * AC * (MS / 16) * (MS / 16) >= 64
+                                                             : FFMP_WGRAD_PREFETCH != 0);
     if constexpr (kPrefetch) {
       // the next k-step's fragments are read while this one's MFMAs run (two register sets, the loop
       // unrolled by two so they swap roles without copies)
@@ -1034,12 +1051,19 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   const int per_chunk = (B + chunks - 1) / chunks;
   const dim3 grid((KH / TKY) * (KW / TKX), (B + per_chunk - 1) / per_chunk);
   if (t_conv_dry) return FFMP_OK;
-  if (ms == 16)
-    hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 16>), grid, dim3(256), bytes(R), s, (const __bf16*)g,
-                       (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
-  else
-    hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 32>), grid, dim3(256), bytes(R), s, (const __bf16*)g,
-                       (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+  auto go = [&](auto MS_, auto PF_) {
+    hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, decltype(MS_)::value, decltype(PF_)::value>), grid, dim3(256),
+                       bytes(R), s, (const __bf16*)g, (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R,
+                       per_chunk);
+  };
+  const bool pf = ffmp_detail::g_conv_wgpf != 0;
+  if (ms == 16) {
+    if (pf) go(std::integral_constant<int, 16>{}, std::true_type{});
+    else go(std::integral_constant<int, 16>{}, std::false_type{});
+  } else {
+    if (pf) go(std::integral_constant<int, 32>{}, std::true_type{});
+    else go(std::integral_constant<int, 32>{}, std::false_type{});
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FFMP_E_HIP, "ffmp_conv2d_wgrad launch: %s", hipGetErrorString(e));
   return FFMP_OK;

@@ -45,6 +45,7 @@ int32_t ring_extra_swap(int32_t v);  // ffmp_ring.hip (FFMP_TUNE_RING_EXTRA)
 int conv_mfma_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_MFMA)
 int conv_kys_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_KYS)
 int conv_lb_swap(int v);             // ffmp_conv.hip (FFMP_TUNE_CONV_LB)
+int conv_wgpf_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_WGPF)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1735,6 +1736,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
     case FFMP_TUNE_CONV_LB:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv B-through-LDS must be 0 or 1");
       return ffmp_detail::conv_lb_swap(value);
+    case FFMP_TUNE_CONV_WGPF:
+      if (value != 0 && value != 1) return fail(FFMP_E_ARG, "weight-gradient prefetch must be 0 or 1");
+      return ffmp_detail::conv_wgpf_swap(value);
     case FFMP_TUNE_RING_EXTRA:
       if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");
       return ffmp_detail::ring_extra_swap(value);

@@ -197,6 +197,8 @@ int64_t ffmp_layout(int32_t which);
                                    1), 1, 2 or 4 (the same products and sums) */
 #define FFMP_TUNE_CONV_LB 9     /* 1: the unpadded row-ring forward shares each tap's weights through LDS
                                    (one barrier per tap); 0 (default): from L1/L2 per wave */
+#define FFMP_TUNE_CONV_WGPF 10  /* 1: the weight gradient reads each k-step's operands during the previous
+                                   one's MFMAs (two register sets); 0 (default): not */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

@@ -117,8 +117,10 @@ __device__ __forceinline__ int2 in_geom(int W, int dx, int flags) {
 // compile-time constants (no per-read address arithmetic, unlike an XOR swizzle).
 template <int C>
 __host__ __device__ __forceinline__ int cell_off(int col) {
-  constexpr int CPR = 256 / (C * 2);  // columns per 256 bytes
-  return col * C * 2 + (col / CPR) * 16;
+  constexpr unsigned CPR = 256 / (C * 2);  // columns per 256 bytes
+  // unsigned: col >= 0 at every call, and a signed division by 4 costs the kernels' inner loops three
+  // VALU per operand address (ashr / lshr / add before the shift)
+  return (int)((unsigned)col * (C * 2) + ((unsigned)col / CPR) * 16);
 }
 template <int C>
 __host__ __device__ __forceinline__ int lds_pitch(int W) {  // bytes of one padded row image
@@ -311,28 +313,61 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
 #pragma unroll
         for (int mb = 0; mb < AM; ++mb) aoff[mb] = ((ypos[mb] + ky) % RING) * pitch;
         // the MFMAs of tap (ky, kx) with its B fragments
-        auto tap = [&](int kx, const bf16x8 (&bt)[AN][KSTEPS]) {
-          // the lane's column of each block, or the zero column outside the tensor (PAD)
-          int abase[AM];
+        // A fragments of tap kx (every k-step, every position block) into registers: all of a tap's
+        // reads are issued before its first MFMA (round 5's loop read one fragment, waited for it and
+        // ran its MFMA, one LDS latency per MFMA: profiles/r06c_conv1_isa.txt)
+        auto read_a = [&](int kx, bf16x8 (&a)[KSTEPS][AM]) {
+          int abase[AM];  // the lane's column of each block, or the zero column outside the tensor (PAD)
 #pragma unroll
           for (int mb = 0; mb < AM; ++mb) {
             const int col = xcol[mb] + kx * dx;
             abase[mb] = (!PAD || (unsigned)col < (unsigned)W ? aoff[mb] + cell_off<C>(col) : zero_off) + kh * 16;
           }
 #pragma unroll
-          for (int s = 0; s < KSTEPS; ++s) {
-            bf16x8 a[AM];
+          for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
-            for (int mb = 0; mb < AM; ++mb) a[mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
+            for (int mb = 0; mb < AM; ++mb) a[s][mb] = *(const bf16x8*)(lds + abase[mb] + s * M::KS * 2);
+        };
+        auto mma_tap = [&](const bf16x8 (&a)[KSTEPS][AM], const bf16x8 (&bt)[AN][KSTEPS]) {
+#pragma unroll
+          for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
             for (int mb = 0; mb < AM; ++mb)
 #pragma unroll
-              for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[mb], bt[nb][s], acc[mb][nb]);
-          }
+              for (int nb = 0; nb < AN; ++nb) acc[mb][nb] = M::mma(a[s][mb], bt[nb][s], acc[mb][nb]);
         };
-        if constexpr (kBAhead == 2) {
+        auto tap = [&](int kx, const bf16x8 (&bt)[AN][KSTEPS]) {
+          bf16x8 a[KSTEPS][AM];
+          read_a(kx, a);
+          mma_tap(a, bt);
+        };
+        // two A register sets where they fit beside the rest (<= 8 fragments a tap: 32 + 32 registers;
+        // the 64-channel padded data-gradient form has 16 and spilled with two sets)
+        constexpr bool kAAhead = KSTEPS * AM <= 8;
+        if constexpr (kBAhead == 2 && kAAhead) {
           // two taps per trip, B in two register sets that swap roles without copies: the next tap's
-          // fragments are requested before this tap's MFMAs and waited for a whole tap later
+          // fragments are requested before this tap's MFMAs and waited for a whole tap later; A the
+          // same way within the kernel row (the next tap's reads in flight during this tap's MFMAs)
+          bf16x8 a0[KSTEPS][AM], a1[KSTEPS][AM];
+          int kx = 0;
+          if (KW > 1) read_a(0, a0);
+          for (; kx + 1 < KW; kx += 2) {
+            load_b(ky * KW + kx + 1, bnx);
+            read_a(kx + 1, a1);
+            mma_tap(a0, bcur);
+            load_b(ky * KW + kx + 2, bcur);
+            if (kx + 2 < KW) read_a(kx + 2, a0);
+            mma_tap(a1, bnx);
+          }
+          if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
+            load_b(ky * KW + kx + 1, bnx);
+            tap(kx, bcur);
+#pragma unroll
+            for (int nb = 0; nb < AN; ++nb)
+#pragma unroll
+              for (int s = 0; s < KSTEPS; ++s) bcur[nb][s] = bnx[nb][s];
+          }
+        } else if constexpr (kBAhead == 2) {
           int kx = 0;
           for (; kx + 1 < KW; kx += 2) {
             load_b(ky * KW + kx + 1, bnx);
@@ -340,7 +375,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
             load_b(ky * KW + kx + 2, bcur);
             tap(kx + 1, bnx);
           }
-          if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
+          if (kx < KW) {
             load_b(ky * KW + kx + 1, bnx);
             tap(kx, bcur);
 #pragma unroll

@@ -61,6 +61,13 @@ int conv_wgpf_swap(int v) {
   g_conv_wgpf = v;
   return prev;
 }
+// conv2-shaped forwards with B fragments two taps ahead (FFMP_TUNE_CONV_BA2): 0 = default (off), 1 = on
+int g_conv_ba2 = 0;
+int conv_ba2_swap(int v) {
+  const int prev = g_conv_ba2;
+  g_conv_ba2 = v;
+  return prev;
+}
 // kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = default (1), 1, 2 or 4
 int g_conv_kys = 0;
 int conv_kys_swap(int v) {
@@ -84,11 +91,11 @@ constexpr int kWaves = 4;
 // global memory: C * 2 (a plain NHWC row), or, for an input folded on the fly (FFMP_CONV_X_FOLD),
 // the unfolded cell's (C / F) * 2 — folded cell x is then the C * 2 bytes starting at unfolded cell
 // x (dword-aligned, read as dwords).
-template <int C>
-__device__ __forceinline__ void load_row_regs(const char* __restrict__ src, int chunks, int cellb, uint4 (&buf)[4]) {
+template <int C, int NR = 4>
+__device__ __forceinline__ void load_row_regs(const char* __restrict__ src, int chunks, int cellb, uint4 (&buf)[NR]) {
   constexpr int CPC = C / 8;  // 16-byte chunks per cell
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int q = threadIdx.x + 256 * i;
     if (q >= chunks) continue;
     if (!src) {
@@ -127,11 +134,11 @@ __host__ __device__ __forceinline__ int lds_pitch(int W) {  // bytes of one padd
   return cell_off<C>(W - 1) + C * 2;
 }
 
-template <int C>
-__device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4 (&buf)[4]) {
+template <int C, int NR = 4>
+__device__ __forceinline__ void store_row_lds(char* dst, int chunks, const uint4 (&buf)[NR]) {
   constexpr int CPC = C / 8;  // 16-byte chunks per column
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int q = threadIdx.x + 256 * i;
     if (q < chunks) *(uint4*)(dst + cell_off<C>(q / CPC) + 16 * (q % CPC)) = buf[i];
   }
@@ -219,7 +226,11 @@ __device__ __forceinline__ bf16x8 load_bfrag_ms(const __bf16* __restrict__ w, in
   }
 }
 
-template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32, int KYS = 1>
+// NRC: 16-byte row chunks per thread the next-row registers hold (ceil(row bytes / 4 KiB); 4 covers
+// every shape, conv2's 4.4 KiB rows need 2: 8 registers fewer); BA: B fragments 1 or 2 taps ahead
+// (0: 2 for one channel block, 1 for two — the 1-ahead set of conv2's forward waits on every tap's
+// loads, the 2-ahead one needs the registers NRC = 2 frees)
+template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32, int KYS = 1, int NRC = 4, int BA = 0>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
         dst[nb][s] = load_bfrag_ms<C, NB, WF, MS>(w, t, nb, s, r, kh);
       }
   };
-  constexpr int kBAhead = FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
+  constexpr int kBAhead = BA > 0 ? BA : FFMP_CONV_BAHEAD > 0 ? FFMP_CONV_BAHEAD : (NB == 1 ? 2 : 1);
   bf16x8 bcur[AN][KSTEPS];
   bf16x8 bnx[AN][KSTEPS];  // kBAhead 2: the ping-pong partner of bcur
   load_b(min(wk_lo, KH - 1) * KW, bcur);
@@ -303,10 +314,10 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
   for (int ky0 = ky_lo; ky0 <= ky_hi; ky0 += KYS) {
     const int kyn = min(KYS, ky_hi - ky0 + 1);
     const int nnext = min(KYS, ky_hi - (ky0 + kyn) + 1);  // rows of the next chunk (<= 0: none)
-    uint4 nrow[KYS][4];
+    uint4 nrow[KYS][NRC];
 #pragma unroll
     for (int j = 0; j < KYS; ++j)
-      if (j < nnext) load_row_regs<C>(row_src(yl + ky0 + kyn + j), chunks, gin.x, nrow[j]);
+      if (j < nnext) load_row_regs<C, NRC>(row_src(yl + ky0 + kyn + j), chunks, gin.x, nrow[j]);
     for (int ky = ky0; ky < ky0 + kyn; ++ky) {
       if (ky >= wk_lo && ky <= wk_hi) {
         int aoff[AM];
@@ -341,9 +352,11 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
           read_a(kx, a);
           mma_tap(a, bt);
         };
-        // two A register sets where they fit beside the rest (<= 8 fragments a tap: 32 + 32 registers;
-        // the 64-channel padded data-gradient form has 16 and spilled with two sets)
-        constexpr bool kAAhead = KSTEPS * AM <= 8;
+        // two A register sets where they fit beside the rest: accumulators + two A sets + two B sets
+        // within 192 of the 256 registers (the 64-channel padded data-gradient form, 16 A fragments a
+        // tap, and conv2's two channel blocks, 128 accumulator registers, spilled with two A sets)
+        constexpr bool kAAhead =
+            AM * AN * (MS * MS / 64) + 2 * 4 * KSTEPS * AM + 2 * 4 * AN * KSTEPS <= 192;
         if constexpr (kBAhead == 2 && kAAhead) {
           // two taps per trip, B in two register sets that swap roles without copies: the next tap's
           // fragments are requested before this tap's MFMAs and waited for a whole tap later; A the
@@ -397,13 +410,13 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
       }
     }
     if constexpr (KYS == 1) {
-      if (nnext > 0) store_row_lds<C>(lds + ((yl + ky0 + 1) % RING) * pitch, chunks, nrow[0]);
+      if (nnext > 0) store_row_lds<C, NRC>(lds + ((yl + ky0 + 1) % RING) * pitch, chunks, nrow[0]);
       __syncthreads();
     } else {
       __syncthreads();  // every wave done with the rows the new ones replace
 #pragma unroll
       for (int j = 0; j < KYS; ++j)
-        if (j < nnext) store_row_lds<C>(lds + ((yl + ky0 + kyn + j) % RING) * pitch, chunks, nrow[j]);
+        if (j < nnext) store_row_lds<C, NRC>(lds + ((yl + ky0 + kyn + j) % RING) * pitch, chunks, nrow[j]);
       __syncthreads();
     }
   }
@@ -776,8 +789,19 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
     }
   }
   if (t_conv_dry) return FFMP_OK;
+  const int chunks = (W * C * 2) / 16;
   auto go = [&](auto MS_, auto KYS_) {
     constexpr int kMS = decltype(MS_)::value, kKYS = decltype(KYS_)::value;
+    // conv2's shape (32 -> 64, unpadded): the two-register-row, B-two-taps-ahead variant where the
+    // row fits (FFMP_TUNE_CONV_BA2: 0 = default, 1 = on, 2 = off)
+    if constexpr (C == 32 && NB == 2 && !PAD && kMS == 32 && kKYS == 1) {
+      const int ba2 = ffmp_detail::g_conv_ba2;
+      if (chunks <= 512 && ba2 == 1) {
+        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 2, 2>), grid, dim3(256), lds, s,
+                           (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+        return;
+      }
+    }
     hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, kMS, kKYS>), grid, dim3(256), lds, s, (const __bf16*)x,
                        (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
   };

@@ -46,6 +46,7 @@ int conv_mfma_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_MFMA)
 int conv_kys_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_KYS)
 int conv_lb_swap(int v);             // ffmp_conv.hip (FFMP_TUNE_CONV_LB)
 int conv_wgpf_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_WGPF)
+int conv_ba2_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_BA2)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1739,6 +1740,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
     case FFMP_TUNE_CONV_WGPF:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "weight-gradient prefetch must be 0 or 1");
       return ffmp_detail::conv_wgpf_swap(value);
+    case FFMP_TUNE_CONV_BA2:
+      if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv B-two-ahead must be 0 or 1");
+      return ffmp_detail::conv_ba2_swap(value);
     case FFMP_TUNE_RING_EXTRA:
       if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");
       return ffmp_detail::ring_extra_swap(value);

@@ -199,6 +199,8 @@ int64_t ffmp_layout(int32_t which);
                                    (one barrier per tap); 0 (default): from L1/L2 per wave */
 #define FFMP_TUNE_CONV_WGPF 10  /* 1: the weight gradient reads each k-step's operands during the previous
                                    one's MFMAs (two register sets); 0 (default): not */
+#define FFMP_TUNE_CONV_BA2 11   /* 1: the 32 -> 64 unpadded row-ring forward (conv2) loads its B fragments two
+                                   taps ahead (rows staged in 2 registers); 0 (default): one tap ahead */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

@@ -27,6 +27,9 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "ffmp.h"
 
@@ -66,6 +69,14 @@ int g_conv_ba2 = 0;
 int conv_ba2_swap(int v) {
   const int prev = g_conv_ba2;
   g_conv_ba2 = v;
+  return prev;
+}
+// 32-position blocks per wave of the row-ring forward (FFMP_TUNE_CONV_MBW): 0 = by the grid-fill
+// model (pick_mbw), 1 / 2 / 3 / 4 forced
+int g_conv_mbw = 0;
+int conv_mbw_swap(int v) {
+  const int prev = g_conv_mbw;
+  g_conv_mbw = v;
   return prev;
 }
 // kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS): 0 = default (1), 1, 2 or 4
@@ -353,10 +364,10 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
           mma_tap(a, bt);
         };
         // two A register sets where they fit beside the rest: accumulators + two A sets + two B sets
-        // within 192 of the 256 registers (the 64-channel padded data-gradient form, 16 A fragments a
+        // within 168 of the 256 registers (the 64-channel padded data-gradient form, 16 A fragments a
         // tap, and conv2's two channel blocks, 128 accumulator registers, spilled with two A sets)
         constexpr bool kAAhead =
-            AM * AN * (MS * MS / 64) + 2 * 4 * KSTEPS * AM + 2 * 4 * AN * KSTEPS <= 192;
+            AM * AN * (MS * MS / 64) + 2 * 4 * KSTEPS * AM + 2 * 4 * AN * KSTEPS <= 168;
         if constexpr (kBAhead == 2 && kAAhead) {
           // two taps per trip, B in two register sets that swap roles without copies: the next tap's
           // fragments are requested before this tap's MFMAs and waited for a whole tap later; A the
@@ -729,29 +740,64 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   return FFMP_OK;
 }
 
-// positions per workgroup: 512 (MBW 4), 256 or 128 — the largest tile (the most reuse of each B
-// fragment) whose rounding of an image's positions costs at most 10 % more than the tightest, and
-// whose ring leaves room for two workgroups per CU
-int pick_mbw(int P, int Wo, size_t slotbytes) {
-  static const int forced = [] {  // FFMP_CONV_MBW = 1 / 2 / 4: a probe knob (tools/conv_variants.py)
+// positions per workgroup: 512 (MBW 4), 384, 256 or 128, by a grid-fill model.  Each candidate tile
+// gives B * ceil(P / PT) workgroups; slots[i] of them run at once (the device's CUs x the kernel's
+// occupancy at that tile's LDS); the launch takes ceil(workgroups / slots) rounds of PT positions
+// each.  The cheapest tile wins, ties to the larger one (more reuse of each B fragment).  Conv2 at
+// B = 256 (1,444 positions, 256 CUs x 2): 512-position tiles are 768 workgroups = 1.5 rounds (the
+// second half-empty), 384-position tiles 1,024 = 2 full rounds of 3/4 the work.  The tiling never
+// changes results (each position's sum runs over the same taps in the same order).
+int pick_mbw(int P, int B, const int (&slots)[4]) {
+  static const int forced_env = [] {  // FFMP_CONV_MBW = 1 / 2 / 3 / 4: a probe knob (tools/conv_variants.py)
     const char* v = getenv("FFMP_CONV_MBW");
     const int m = v ? atoi(v) : 0;
-    return (m == 1 || m == 2 || m == 4) ? m : 0;
+    return (m >= 1 && m <= 4) ? m : 0;
   }();
+  const int forced = ffmp_detail::g_conv_mbw ? ffmp_detail::g_conv_mbw : forced_env;
   if (forced) return forced;
-  long padded[3], least = -1;
-  const int mbws[3] = {4, 2, 1};
-  for (int i = 0; i < 3; ++i) {
-    const int pt = kWaves * mbws[i] * 32;
-    padded[i] = (long)((P + pt - 1) / pt) * pt;
-    if (least < 0 || padded[i] < least) least = padded[i];
+  const int mbws[4] = {4, 3, 2, 1};
+  long best = -1;
+  int pick = 1;
+  for (int i = 0; i < 4; ++i) {
+    if (slots[i] <= 0) continue;  // the ring does not fit
+    const long pt = kWaves * mbws[i] * 32;
+    const long wgs = (long)B * ((P + pt - 1) / pt);
+    const long cost = (wgs + slots[i] - 1) / slots[i] * pt;
+    if (best < 0 || cost < best) best = cost, pick = mbws[i];
   }
-  for (int i = 0; i < 3; ++i) {
-    const int pt = kWaves * mbws[i] * 32;
-    const size_t ring = (size_t)((pt + Wo - 1) / Wo + 2) * slotbytes;
-    if ((ring <= 80 * 1024 || mbws[i] == 1) && padded[i] * 10 <= least * 11) return mbws[i];
+  return pick;
+}
+
+// CUs of the current device (256 on MI355X; that, when there is none: the dry-run shape checks)
+int device_cus() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev] = n;
+  return n;
+}
+
+// workgroups of a kernel resident per CU at `lds` bytes of dynamic LDS (2 when the runtime cannot say)
+int wgs_per_cu(const void* fn, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(fn, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, lds) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    n = 2;
   }
-  return 1;
+  cache[key] = n;
+  return n;
 }
 
 template <int C, int NB, int MBW, bool PAD, bool WF>
@@ -809,7 +855,9 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
     if (ffmp_detail::mfma_for(32) == 16) go(std::integral_constant<int, 16>{}, KYS_);
     else go(std::integral_constant<int, 32>{}, KYS_);
   };
-  if constexpr (NB == 1) {
+  if constexpr (MBW == 3) {  // built for the default launch only (pick_mbw offers it for no other)
+    go(std::integral_constant<int, 32>{}, std::integral_constant<int, 1>{});
+  } else if constexpr (NB == 1) {
     if (kys == 4) with_ms(std::integral_constant<int, 4>{});
     else if (kys == 2) with_ms(std::integral_constant<int, 2>{});
     else with_ms(std::integral_constant<int, 1>{});
@@ -822,6 +870,23 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   return FFMP_OK;
 }
 
+// the default launch of launch_fwd_mbw (KYS 1, the configured MFMA shape): workgroups per CU, 0 when
+// its ring exceeds the LDS
+template <int C, int NB, int MBW, bool PAD, bool WF>
+int fwd_occupancy(int W, int Wo) {
+  constexpr int PT = kWaves * MBW * 32;
+  const size_t lds = (size_t)((PT + Wo - 1) / Wo + 2) * lds_pitch<C>(W) + C * 2;
+  if (lds > 160 * 1024) return 0;
+  if constexpr (MBW == 3) {  // the default launch only (32x32x16, one kernel row per ring step)
+    if (ffmp_detail::mfma_for(32) != 32 || ffmp_detail::g_conv_kys > 1) return 0;
+    return wgs_per_cu((const void*)conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1>, lds);
+  } else {
+    const void* fn = ffmp_detail::mfma_for(32) == 16 ? (const void*)conv_fwd_kernel<C, NB, MBW, PAD, WF, 16, 1>
+                                                     : (const void*)conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1>;
+    return wgs_per_cu(fn, lds);
+  }
+}
+
 template <int C, int NB, bool PAD, bool WF>
 int launch_fwd_wf(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int KH, int KW, int pad,
                int dx, int flags, hipStream_t s) {
@@ -829,8 +894,19 @@ int launch_fwd_wf(const void* x, const void* w, const float* bias, void* y, int 
   // small images with a kernel deep enough to split over the waves: conv_small_kernel
   if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= 76 * 1024 && (W * C * 2) % 16 == 0)
     return launch_small<C, NB, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-  switch (pick_mbw(Ho * Wo, Wo, (size_t)lds_pitch<C>(W))) {
+  int slots[4];
+  if (t_conv_dry) {
+    slots[0] = slots[1] = slots[2] = slots[3] = 512;
+  } else {
+    const int cus = device_cus();
+    slots[0] = cus * fwd_occupancy<C, NB, 4, PAD, WF>(W, Wo);
+    slots[1] = cus * fwd_occupancy<C, NB, 3, PAD, WF>(W, Wo);
+    slots[2] = cus * fwd_occupancy<C, NB, 2, PAD, WF>(W, Wo);
+    slots[3] = cus * fwd_occupancy<C, NB, 1, PAD, WF>(W, Wo);
+  }
+  switch (pick_mbw(Ho * Wo, B, slots)) {
     case 4: return launch_fwd_mbw<C, NB, 4, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
+    case 3: return launch_fwd_mbw<C, NB, 3, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     case 2: return launch_fwd_mbw<C, NB, 2, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     default: return launch_fwd_mbw<C, NB, 1, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
   }

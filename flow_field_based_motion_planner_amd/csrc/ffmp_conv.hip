@@ -740,14 +740,18 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   return FFMP_OK;
 }
 
-// positions per workgroup: 512 (MBW 4), 384, 256 or 128, by a grid-fill model.  Each candidate tile
-// gives B * ceil(P / PT) workgroups; slots[i] of them run at once (the device's CUs x the kernel's
-// occupancy at that tile's LDS); the launch takes ceil(workgroups / slots) rounds of PT positions
-// each.  The cheapest tile wins, ties to the larger one (more reuse of each B fragment).  Conv2 at
-// B = 256 (1,444 positions, 256 CUs x 2): 512-position tiles are 768 workgroups = 1.5 rounds (the
-// second half-empty), 384-position tiles 1,024 = 2 full rounds of 3/4 the work.  The tiling never
-// changes results (each position's sum runs over the same taps in the same order).
-int pick_mbw(int P, int B, const int (&slots)[4]) {
+// positions per workgroup: 512 (MBW 4), 384, 256 or 128.  First the largest tile (the most reuse of
+// each B fragment) whose rounding of an image's positions costs at most 10 % more than the tightest
+// and whose ring leaves room for two workgroups per CU.  Then, when that is the 512-position tile, a
+// grid-fill check against the 384-position one: B * ceil(P / PT) workgroups in rounds of `slots`
+// (CUs x the kernel's occupancy at that tile's LDS); a round costs PT x its workgroups per CU, a
+// partial last round with a fraction f of the slots 0.3 + 0.7 f of a full one (its CUs run fewer
+// waves, at a lower rate), and the 384-position tile's per-position rate is 0.96 of the 512's (less
+// reuse; profiles/r06e_conv_ab*.txt).  Conv2 at B = 256 (1,444 positions, 2 per CU on 256 CUs): 512
+// tiles = 768 workgroups = 1.5 rounds, 384 tiles = 1,024 = 2 full rounds: 1.19 vs 1.23 ms; at B =
+// 1,024 both fill their rounds and the 512 tile stays (4.50 vs 4.70 ms).  Never changes results
+// (each position's sum runs over the same taps in the same order).
+int pick_mbw(int P, int Wo, size_t slotbytes, int B, int slots4, int slots3) {
   static const int forced_env = [] {  // FFMP_CONV_MBW = 1 / 2 / 3 / 4: a probe knob (tools/conv_variants.py)
     const char* v = getenv("FFMP_CONV_MBW");
     const int m = v ? atoi(v) : 0;
@@ -755,17 +759,29 @@ int pick_mbw(int P, int B, const int (&slots)[4]) {
   }();
   const int forced = ffmp_detail::g_conv_mbw ? ffmp_detail::g_conv_mbw : forced_env;
   if (forced) return forced;
-  const int mbws[4] = {4, 3, 2, 1};
-  long best = -1;
-  int pick = 1;
-  for (int i = 0; i < 4; ++i) {
-    if (slots[i] <= 0) continue;  // the ring does not fit
-    const long pt = kWaves * mbws[i] * 32;
-    const long wgs = (long)B * ((P + pt - 1) / pt);
-    const long cost = (wgs + slots[i] - 1) / slots[i] * pt;
-    if (best < 0 || cost < best) best = cost, pick = mbws[i];
+  long padded[3], least = -1;
+  const int mbws[3] = {4, 2, 1};
+  for (int i = 0; i < 3; ++i) {
+    const int pt = kWaves * mbws[i] * 32;
+    padded[i] = (long)((P + pt - 1) / pt) * pt;
+    if (least < 0 || padded[i] < least) least = padded[i];
   }
-  return pick;
+  int pick = 1;
+  for (int i = 0; i < 3; ++i) {
+    const int pt = kWaves * mbws[i] * 32;
+    const size_t ring = (size_t)((pt + Wo - 1) / Wo + 2) * slotbytes;
+    if ((ring <= 80 * 1024 || mbws[i] == 1) && padded[i] * 10 <= least * 11) {
+      pick = mbws[i];
+      break;
+    }
+  }
+  if (pick != 4 || slots4 <= 0 || slots3 <= 0) return pick;
+  auto cost = [&](int mbw, int slots, double eff) {
+    const long pt = kWaves * mbw * 32;
+    const double wgs = (double)B * (double)((P + pt - 1) / pt), r = wgs / slots, full = (double)(long)r, f = r - full;
+    return (full + (f > 0 ? 0.3 + 0.7 * f : 0.0)) * (double)pt * (double)slots / eff;
+  };
+  return cost(3, slots3, 0.96) < cost(4, slots4, 1.0) ? 3 : 4;
 }
 
 // CUs of the current device (256 on MI355X; that, when there is none: the dry-run shape checks)
@@ -894,17 +910,17 @@ int launch_fwd_wf(const void* x, const void* w, const float* bias, void* y, int 
   // small images with a kernel deep enough to split over the waves: conv_small_kernel
   if (Ho * Wo <= 2048 && KH >= 4 && small_window_bytes(Wo, KH, W, C) <= 76 * 1024 && (W * C * 2) % 16 == 0)
     return launch_small<C, NB, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
-  int slots[4];
-  if (t_conv_dry) {
-    slots[0] = slots[1] = slots[2] = slots[3] = 512;
-  } else {
+  int slots4 = 0, slots3 = 0;  // 0: no grid-fill check (the dry-run shape checks, one channel block)
+  if (!t_conv_dry) {
     const int cus = device_cus();
-    slots[0] = cus * fwd_occupancy<C, NB, 4, PAD, WF>(W, Wo);
-    slots[1] = cus * fwd_occupancy<C, NB, 3, PAD, WF>(W, Wo);
-    slots[2] = cus * fwd_occupancy<C, NB, 2, PAD, WF>(W, Wo);
-    slots[3] = cus * fwd_occupancy<C, NB, 1, PAD, WF>(W, Wo);
+    if constexpr (NB == 2) {  // measured for the two-channel-block layers only (conv2's forward);
+      // the folded conv1 (one block) ran 8 % slower on 384 tiles at 2 workgroups per CU than on 512
+      // at 3, which the model above does not see
+      slots4 = cus * fwd_occupancy<C, NB, 4, PAD, WF>(W, Wo);
+      slots3 = cus * fwd_occupancy<C, NB, 3, PAD, WF>(W, Wo);
+    }
   }
-  switch (pick_mbw(Ho * Wo, B, slots)) {
+  switch (pick_mbw(Ho * Wo, Wo, (size_t)lds_pitch<C>(W), B, slots4, slots3)) {
     case 4: return launch_fwd_mbw<C, NB, 4, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     case 3: return launch_fwd_mbw<C, NB, 3, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);
     case 2: return launch_fwd_mbw<C, NB, 2, PAD, WF>(x, w, bias, y, B, H, W, KH, KW, pad, dx, flags, s);

@@ -64,7 +64,8 @@ int conv_wgpf_swap(int v) {
   g_conv_wgpf = v;
   return prev;
 }
-// conv2-shaped forwards with B fragments two taps ahead (FFMP_TUNE_CONV_BA2): 0 = default (off), 1 = on
+// conv2-shaped forwards with pinned load schedules (FFMP_TUNE_CONV_BA2): 0 = default (off), 1 = B
+// fragments two taps ahead, 2 = one tap ahead
 int g_conv_ba2 = 0;
 int conv_ba2_swap(int v) {
   const int prev = g_conv_ba2;
@@ -240,8 +241,10 @@ __device__ __forceinline__ bf16x8 load_bfrag_ms(const __bf16* __restrict__ w, in
 // NRC: 16-byte row chunks per thread the next-row registers hold (ceil(row bytes / 4 KiB); 4 covers
 // every shape, conv2's 4.4 KiB rows need 2: 8 registers fewer); BA: B fragments 1 or 2 taps ahead
 // (0: 2 for one channel block, 1 for two — the 1-ahead set of conv2's forward waits on every tap's
-// loads, the 2-ahead one needs the registers NRC = 2 frees)
-template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32, int KYS = 1, int NRC = 4, int BA = 0>
+// loads, the 2-ahead one needs the registers NRC = 2 frees); PIN: each tap's loads pinned ahead of
+// its MFMAs by scheduling barriers (the scheduler otherwise sinks the next tap's B loads below half
+// of the tap's MFMAs and waits on each A read one MFMA after issuing it: profiles/r06e_conv2_isa.txt)
+template <int C, int NB, int MBW, bool PAD, bool WF, int MS = 32, int KYS = 1, int NRC = 4, int BA = 0, bool PIN = false>
 __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ w,
                                                           const float* __restrict__ bias, void* __restrict__ y, int H,
                                                           int W, int KH, int KW, int pad, int dx, int RING, int flags) {
@@ -368,6 +371,9 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
         // tap, and conv2's two channel blocks, 128 accumulator registers, spilled with two A sets)
         constexpr bool kAAhead =
             AM * AN * (MS * MS / 64) + 2 * 4 * KSTEPS * AM + 2 * 4 * AN * KSTEPS <= 168;
+        auto pin = [] {
+          if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+        };
         if constexpr (kBAhead == 2 && kAAhead) {
           // two taps per trip, B in two register sets that swap roles without copies: the next tap's
           // fragments are requested before this tap's MFMAs and waited for a whole tap later; A the
@@ -378,10 +384,14 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
           for (; kx + 1 < KW; kx += 2) {
             load_b(ky * KW + kx + 1, bnx);
             read_a(kx + 1, a1);
+            pin();
             mma_tap(a0, bcur);
+            pin();
             load_b(ky * KW + kx + 2, bcur);
             if (kx + 2 < KW) read_a(kx + 2, a0);
+            pin();
             mma_tap(a1, bnx);
+            pin();
           }
           if (kx < KW) {  // odd KW: the last tap, then its successor's fragments back into bcur
             load_b(ky * KW + kx + 1, bnx);
@@ -394,10 +404,17 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
         } else if constexpr (kBAhead == 2) {
           int kx = 0;
           for (; kx + 1 < KW; kx += 2) {
+            bf16x8 a[KSTEPS][AM];
             load_b(ky * KW + kx + 1, bnx);
-            tap(kx, bcur);
+            read_a(kx, a);
+            pin();
+            mma_tap(a, bcur);
+            pin();
             load_b(ky * KW + kx + 2, bcur);
-            tap(kx + 1, bnx);
+            read_a(kx + 1, a);
+            pin();
+            mma_tap(a, bnx);
+            pin();
           }
           if (kx < KW) {
             load_b(ky * KW + kx + 1, bnx);
@@ -410,8 +427,12 @@ __global__ __launch_bounds__(256, FFMP_CONV_FWD_OCC) void conv_fwd_kernel(const 
         } else {
           for (int kx = 0; kx < KW; ++kx) {
             bf16x8 bnext[AN][KSTEPS];
+            bf16x8 a[KSTEPS][AM];
             load_b(ky * KW + kx + 1, bnext);
-            tap(kx, bcur);
+            read_a(kx, a);
+            pin();
+            mma_tap(a, bcur);
+            pin();
 #pragma unroll
             for (int nb = 0; nb < AN; ++nb)
 #pragma unroll
@@ -854,12 +875,17 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   const int chunks = (W * C * 2) / 16;
   auto go = [&](auto MS_, auto KYS_) {
     constexpr int kMS = decltype(MS_)::value, kKYS = decltype(KYS_)::value;
-    // conv2's shape (32 -> 64, unpadded): the two-register-row, B-two-taps-ahead variant where the
-    // row fits (FFMP_TUNE_CONV_BA2: 0 = default, 1 = on, 2 = off)
+    // conv2's shape (32 -> 64, unpadded): the pinned-schedule variants (FFMP_TUNE_CONV_BA2: 1 = B two
+    // taps ahead with rows in 2 registers where the row fits, 2 = B one tap ahead)
     if constexpr (C == 32 && NB == 2 && !PAD && kMS == 32 && kKYS == 1) {
       const int ba2 = ffmp_detail::g_conv_ba2;
       if (chunks <= 512 && ba2 == 1) {
-        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 2, 2>), grid, dim3(256), lds, s,
+        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 2, 2, true>), grid, dim3(256), lds, s,
+                           (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+        return;
+      }
+      if (ba2 == 2) {
+        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 4, 1, true>), grid, dim3(256), lds, s,
                            (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
         return;
       }

@@ -1745,7 +1745,7 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       if (value < 0 || value > 4) return fail(FFMP_E_ARG, "conv blocks per wave must be 0-4");
       return ffmp_detail::conv_mbw_swap(value);
     case FFMP_TUNE_CONV_BA2:
-      if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv B-two-ahead must be 0 or 1");
+      if (value < 0 || value > 2) return fail(FFMP_E_ARG, "conv pinned-schedule variant must be 0-2");
       return ffmp_detail::conv_ba2_swap(value);
     case FFMP_TUNE_RING_EXTRA:
       if (value < 0) return fail(FFMP_E_ARG, "ring extra pieces: 0 (default) or 1 + the cap");

@@ -199,8 +199,9 @@ int64_t ffmp_layout(int32_t which);
                                    (one barrier per tap); 0 (default): from L1/L2 per wave */
 #define FFMP_TUNE_CONV_WGPF 10  /* 1: the weight gradient reads each k-step's operands during the previous
                                    one's MFMAs (two register sets); 0 (default): not */
-#define FFMP_TUNE_CONV_BA2 11   /* 1: the 32 -> 64 unpadded row-ring forward (conv2) loads its B fragments two
-                                   taps ahead (rows staged in 2 registers); 0 (default): one tap ahead */
+#define FFMP_TUNE_CONV_BA2 11   /* the 32 -> 64 unpadded row-ring forward (conv2) with each tap's loads pinned
+                                   ahead of its MFMAs: 1 = B fragments two taps ahead (rows staged in 2
+                                   registers), 2 = one tap ahead; 0 (default): the compiler's schedule */
 #define FFMP_TUNE_CONV_MBW 12   /* 32-position blocks per wave of the row-ring forward: 0 (default) = by the
                                    grid-fill model (tiles of 512 / 384 / 256 / 128 positions), 1-4 forced */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);

@@ -292,7 +292,7 @@ def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, d
     conv_knobs(32, 1, 0)
     base = conv2d_nhwc(xb, wp, bias, pad=pad, dx=dx)
     for mfma, kys, lb, ba2, mbw in [(32, 1, 0, 0, 0), (32, 2, 0, 0, 0), (32, 4, 0, 0, 0), (32, 1, 1, 0, 0),
-                                    (32, 1, 0, 1, 0), (32, 1, 0, 0, 1), (32, 1, 0, 0, 2), (32, 1, 0, 0, 3),
+                                    (32, 1, 0, 1, 0), (32, 1, 0, 2, 0), (32, 1, 0, 1, 3), (32, 1, 0, 2, 3), (32, 1, 0, 0, 1), (32, 1, 0, 0, 2), (32, 1, 0, 0, 3),
                                     (32, 1, 0, 0, 4), (16, 1, 0, 0, 0), (16, 4, 0, 0, 0), (0, 0, 0, 0, 0)]:
         conv_knobs(mfma, kys, lb, ba2, mbw)
         for wk in (wp, frag_order(wp)):

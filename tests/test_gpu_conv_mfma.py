@@ -258,12 +258,13 @@ def conv_knobs():
     from flow_field_based_motion_planner_amd import _abi
     lib = _abi.load()
 
-    def setk(mfma=0, kys=0, lb=0, ba2=0, mbw=0):
+    def setk(mfma=0, kys=0, lb=0, ba2=0, mbw=0, planar=0):
         lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, mfma)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_KYS, kys)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_LB, lb)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_BA2, ba2)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_MBW, mbw)
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_PLANAR, planar)
     yield setk
     setk()
 
@@ -276,7 +277,7 @@ def conv_knobs():
     (2, 12, 12, 64, 2, 64, 1, 1), (5, 33, 70, 32, 2, 64, 0, 1), (2, 40, 45, 32, 5, 32, 0, 1)])
 def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, dx):
     """Every launch variant of the forward (FFMP_TUNE_CONV_MFMA 16 / 32, FFMP_TUNE_CONV_KYS 1 / 2 / 4,
-    FFMP_TUNE_CONV_LB, FFMP_TUNE_CONV_BA2, FFMP_TUNE_CONV_MBW 1-4) against float64 within the forward's tolerance; the variants that keep the
+    FFMP_TUNE_CONV_LB, FFMP_TUNE_CONV_BA2, FFMP_TUNE_CONV_MBW 1-4, FFMP_TUNE_CONV_PLANAR) against float64 within the forward's tolerance; the variants that keep the
     32x32x16 accumulation order (kernel rows per ring step, B through LDS) bit-identical to the default."""
     g = torch.Generator(device=DEV).manual_seed(B + H + K + pad)
     xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)
@@ -299,9 +300,9 @@ def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, d
             y = conv2d_nhwc(xb, wk, bias, pad=pad, dx=dx)
             err = (y.double() - ref).abs()
             bad = err > 5e-5 * absref + 1e-6
-            assert not bool(bad.any()), (mfma, kys, lb, ba2, mbw, int(bad.sum()), float(err.max()))
+            assert not bool(bad.any()), (mfma, kys, lb, ba2, mbw, planar, int(bad.sum()), float(err.max()))
             if mfma in (0, 32):  # the default forward keeps 32x32x16
-                assert torch.equal(y, base), (mfma, kys, lb, ba2, mbw)
+                assert torch.equal(y, base), (mfma, kys, lb, ba2, mbw, planar)
 
 
 @pytest.mark.parametrize("mfma", [16, 32])

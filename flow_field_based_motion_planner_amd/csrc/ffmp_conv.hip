@@ -72,6 +72,13 @@ int conv_ba2_swap(int v) {
   g_conv_ba2 = v;
   return prev;
 }
+// the row-ring forward's default launch with pinned load schedules (FFMP_TUNE_CONV_PIN): 0 = off, 1 = on
+int g_conv_pin = 0;
+int conv_pin_swap(int v) {
+  const int prev = g_conv_pin;
+  g_conv_pin = v;
+  return prev;
+}
 // planar ring slots for the row-ring forward (FFMP_TUNE_CONV_PLANAR): 0 = off (default), 1 = on
 int g_conv_planar = 0;
 int conv_planar_swap(int v) {
@@ -940,6 +947,11 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
   auto go = [&](auto MS_, auto KYS_) {
     constexpr int kMS = decltype(MS_)::value, kKYS = decltype(KYS_)::value;
     if constexpr (kMS == 32 && kKYS == 1) {
+      if (ffmp_detail::g_conv_pin == 1 && !planar) {
+        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 4, 0, true, false>), grid, dim3(256), lds, s,
+                           (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+        return;
+      }
       if (planar) {
         hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, 1, 4, 0, false, true>), grid, dim3(256), lds, s,
                            (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);

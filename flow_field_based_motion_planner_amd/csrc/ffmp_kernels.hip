@@ -49,6 +49,7 @@ int conv_wgpf_swap(int v);           // ffmp_conv.hip (FFMP_TUNE_CONV_WGPF)
 int conv_ba2_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_BA2)
 int conv_mbw_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_MBW)
 int conv_planar_swap(int v);         // ffmp_conv.hip (FFMP_TUNE_CONV_PLANAR)
+int conv_pin_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_PIN)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1742,6 +1743,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
     case FFMP_TUNE_CONV_WGPF:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "weight-gradient prefetch must be 0 or 1");
       return ffmp_detail::conv_wgpf_swap(value);
+    case FFMP_TUNE_CONV_PIN:
+      if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv pinned schedule must be 0 or 1");
+      return ffmp_detail::conv_pin_swap(value);
     case FFMP_TUNE_CONV_PLANAR:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv planar slots must be 0 or 1");
       return ffmp_detail::conv_planar_swap(value);

@@ -206,6 +206,8 @@ int64_t ffmp_layout(int32_t which);
                                    grid-fill model (tiles of 512 / 384 / 256 / 128 positions), 1-4 forced */
 #define FFMP_TUNE_CONV_PLANAR 13 /* 1: the row-ring forward keeps each 16-byte channel chunk of a row in a plane of
                                    its own (conflict-free A reads for any first column); 0 (default): padded cells */
+#define FFMP_TUNE_CONV_PIN 14   /* 1: the row-ring forward's default launch with each half-trip's loads pinned ahead
+                                   of its MFMAs by scheduling barriers; 0 (default): the compiler's schedule */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

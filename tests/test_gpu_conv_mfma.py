@@ -258,13 +258,14 @@ def conv_knobs():
     from flow_field_based_motion_planner_amd import _abi
     lib = _abi.load()
 
-    def setk(mfma=0, kys=0, lb=0, ba2=0, mbw=0, planar=0):
+    def setk(mfma=0, kys=0, lb=0, ba2=0, mbw=0, planar=0, pin=0):
         lib.ffmp_set_tuning(_abi.TUNE_CONV_MFMA, mfma)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_KYS, kys)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_LB, lb)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_BA2, ba2)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_MBW, mbw)
         lib.ffmp_set_tuning(_abi.TUNE_CONV_PLANAR, planar)
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_PIN, pin)
     yield setk
     setk()
 
@@ -277,7 +278,7 @@ def conv_knobs():
     (2, 12, 12, 64, 2, 64, 1, 1), (5, 33, 70, 32, 2, 64, 0, 1), (2, 40, 45, 32, 5, 32, 0, 1)])
 def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, dx):
     """Every launch variant of the forward (FFMP_TUNE_CONV_MFMA 16 / 32, FFMP_TUNE_CONV_KYS 1 / 2 / 4,
-    FFMP_TUNE_CONV_LB, FFMP_TUNE_CONV_BA2, FFMP_TUNE_CONV_MBW 1-4, FFMP_TUNE_CONV_PLANAR) against float64 within the forward's tolerance; the variants that keep the
+    FFMP_TUNE_CONV_LB, FFMP_TUNE_CONV_BA2, FFMP_TUNE_CONV_MBW 1-4, FFMP_TUNE_CONV_PLANAR, FFMP_TUNE_CONV_PIN) against float64 within the forward's tolerance; the variants that keep the
     32x32x16 accumulation order (kernel rows per ring step, B through LDS) bit-identical to the default."""
     g = torch.Generator(device=DEV).manual_seed(B + H + K + pad)
     xb = torch.randn((B, H, W, C), device=DEV, generator=g).to(torch.bfloat16)
@@ -292,17 +293,22 @@ def test_conv_launch_variants_match_float64(conv_knobs, B, H, W, C, K, N, pad, d
         absref = F.conv2d(x64.abs(), w64.abs(), padding=pad, dilation=(1, dx)).permute(0, 2, 3, 1)
     conv_knobs(32, 1, 0)
     base = conv2d_nhwc(xb, wp, bias, pad=pad, dx=dx)
-    for mfma, kys, lb, ba2, mbw in [(32, 1, 0, 0, 0), (32, 2, 0, 0, 0), (32, 4, 0, 0, 0), (32, 1, 1, 0, 0),
-                                    (32, 1, 0, 1, 0), (32, 1, 0, 2, 0), (32, 1, 0, 1, 3), (32, 1, 0, 2, 3), (32, 1, 0, 0, 1), (32, 1, 0, 0, 2), (32, 1, 0, 0, 3),
-                                    (32, 1, 0, 0, 4), (16, 1, 0, 0, 0), (16, 4, 0, 0, 0), (0, 0, 0, 0, 0)]:
-        conv_knobs(mfma, kys, lb, ba2, mbw)
+    variants = [  # (mfma, kys, lb, ba2, mbw, planar, pin)
+        (32, 1, 0, 0, 0, 0, 0), (32, 2, 0, 0, 0, 0, 0), (32, 4, 0, 0, 0, 0, 0), (32, 1, 1, 0, 0, 0, 0),
+        (32, 1, 0, 1, 0, 0, 0), (32, 1, 0, 2, 0, 0, 0), (32, 1, 0, 1, 3, 0, 0), (32, 1, 0, 2, 3, 0, 0),
+        (32, 1, 0, 0, 1, 0, 0), (32, 1, 0, 0, 2, 0, 0), (32, 1, 0, 0, 3, 0, 0), (32, 1, 0, 0, 4, 0, 0),
+        (32, 1, 0, 0, 0, 1, 0), (32, 1, 0, 0, 1, 1, 0), (32, 1, 0, 0, 3, 1, 0), (32, 1, 0, 0, 4, 1, 0),
+        (32, 1, 0, 0, 0, 0, 1), (32, 1, 0, 0, 3, 0, 1), (32, 1, 0, 0, 4, 0, 1),
+        (16, 1, 0, 0, 0, 0, 0), (16, 4, 0, 0, 0, 0, 0), (0, 0, 0, 0, 0, 0, 0)]
+    for mfma, kys, lb, ba2, mbw, planar, pin in variants:
+        conv_knobs(mfma, kys, lb, ba2, mbw, planar, pin)
         for wk in (wp, frag_order(wp)):
             y = conv2d_nhwc(xb, wk, bias, pad=pad, dx=dx)
             err = (y.double() - ref).abs()
             bad = err > 5e-5 * absref + 1e-6
-            assert not bool(bad.any()), (mfma, kys, lb, ba2, mbw, planar, int(bad.sum()), float(err.max()))
+            assert not bool(bad.any()), (mfma, kys, lb, ba2, mbw, planar, pin, int(bad.sum()), float(err.max()))
             if mfma in (0, 32):  # the default forward keeps 32x32x16
-                assert torch.equal(y, base), (mfma, kys, lb, ba2, mbw, planar)
+                assert torch.equal(y, base), (mfma, kys, lb, ba2, mbw, planar, pin)
 
 
 @pytest.mark.parametrize("mfma", [16, 32])

@@ -215,7 +215,7 @@ def verify_layout(lib: Optional[C.CDLL] = None) -> None:
 TUNE_RASTER_CPB, TUNE_RASTER_NT, TUNE_RASTER_XCD, TUNE_ENV_WAVES, TUNE_ENV_LANES, TUNE_RING_EXTRA = 1, 2, 3, 4, 5, 6
 TUNE_CONV_MFMA, TUNE_CONV_KYS, TUNE_CONV_LB, TUNE_CONV_WGPF, TUNE_CONV_BA2, TUNE_CONV_MBW, TUNE_CONV_PLANAR = (
     7, 8, 9, 10, 11, 12, 13)
-TUNE_CONV_PIN = 14
+TUNE_CONV_PIN, TUNE_CONV_WGDMA = 14, 15
 RASTER_NT, RASTER_PLAIN, RASTER_XCD, RASTER_NEWEST = 1, 2, 4, 8
 RASTER_TILE2, RASTER_TILE4, RASTER_TILE8 = 16, 32, 64
 RASTER_NARROW = 128  # FFMP_OBS_U8F16: 4 cells per lane instead of 16

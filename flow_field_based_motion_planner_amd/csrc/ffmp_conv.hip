@@ -79,6 +79,14 @@ int conv_pin_swap(int v) {
   g_conv_pin = v;
   return prev;
 }
+// the weight gradient's LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA): 0 = off, 1 = on, 2 = on with
+// the k-step prefetch
+int g_conv_wgdma = 0;
+int conv_wgdma_swap(int v) {
+  const int prev = g_conv_wgdma;
+  g_conv_wgdma = v;
+  return prev;
+}
 // planar ring slots for the row-ring forward (FFMP_TUNE_CONV_PLANAR): 0 = off (default), 1 = on
 int g_conv_planar = 0;
 int conv_planar_swap(int v) {
@@ -1115,7 +1123,13 @@ constexpr int kWgradPieces = 12;  // 16-byte pieces of one stage per thread (<= 
 #ifndef FFMP_WGRAD_PREFETCH
 #define FFMP_WGRAD_PREFETCH 0
 #endif
-template <int C, int N, int TW, int MS = 32, bool PF = false>
+// DMA (FFMP_TUNE_CONV_WGDMA): each stage is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// no staging registers) into one of TWO stage buffers, issued right after the stage's single barrier
+// and landed during the previous stage's k-loop: no store phase, one barrier per stage instead of two,
+// and the 48 staging registers free for the k-step prefetch (PF).  The LDS images stay as above: an
+// LDS-DMA destination is wave-uniform base + 16 x lane, so each lane fetches the source chunk that
+// the swizzled image holds at its linear position (the XOR is its own inverse).
+template <int C, int N, int TW, int MS = 32, bool PF = false, bool DMA = false>
 __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void conv_wgrad_kernel(const __bf16* __restrict__ g, const __bf16* __restrict__ x,
                                                             float* __restrict__ part, int B, int H, int W, int KH,
                                                             int KW, int dx, int TKY, int TKX, int R, int per_chunk) {
@@ -1135,6 +1149,7 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
   const int gh = MS == 32 ? (lane >> 4) & 1 : 0;        // 32x32x16: the 16-column half of the 32
   const int grow = N * 2, xrowb = C * 2;             // image row bytes
   const int Pmax = R * Wo;                            // positions of a full stage
+  const int SB = (Pmax + KP) * grow + (R + TKY - 1) * W * xrowb;  // one stage buffer (DMA: two)
   char* gimg = lds;
   char* ximg = lds + (Pmax + KP) * grow;              // g image + KP zero rows (k-steps past the stage end)
 
@@ -1148,7 +1163,32 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
     dkx[t] = (kxA + k % TKX) * dx;
     toff[t] = (dky[t] * W + dkx[t]) * (C * 2);  // byte offset of tap t's x row (unswizzled images)
   }
-  for (int i = threadIdx.x; i < grow * KP / 16; i += 256) *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x; i < grow * KP / 16; i += 256) {
+    *(uint4*)(gimg + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
+    if constexpr (DMA) *(uint4*)(gimg + SB + Pmax * grow + 16 * i) = uint4{0u, 0u, 0u, 0u};
+  }
+  // DMA: stage (gs, xs: gq g chunks, xq x chunks) into buffer `buf`; wave w issues the 64-chunk groups
+  // w, w + 4, ... of each image (lanes past its end masked off)
+  auto dma_stage = [&](int buf, const char* gs, const char* xs, int gq_, int xq_) {
+    char* gb = lds + buf * SB;
+    char* xb = gb + (Pmax + KP) * grow;
+    for (int k0 = wave * 64; k0 < gq_; k0 += 256) {
+      const int k = k0 + lane;
+      if (k < gq_) {
+        const int row = k / (grow / 16), c = k % (grow / 16);
+        const int cs = N == 64 ? c ^ (swz128(row) >> 4) : c;
+        __builtin_amdgcn_global_load_lds((const void*)(gs + (size_t)row * grow + 16 * cs), (__attribute__((address_space(3))) void*)(gb + 16 * k0), 16, 0, 0);
+      }
+    }
+    for (int k0 = wave * 64; k0 < xq_; k0 += 256) {
+      const int k = k0 + lane;
+      if (k < xq_) {
+        const int row = k / (xrowb / 16), c = k % (xrowb / 16);
+        const int cs = C == 64 ? c ^ (swz128(row) >> 4) : c;
+        __builtin_amdgcn_global_load_lds((const void*)(xs + (size_t)row * xrowb + 16 * cs), (__attribute__((address_space(3))) void*)(xb + 16 * k0), 16, 0, 0);
+      }
+    }
+  };
 
   typename M::acc_t acc[TW][AN][AC];
 #pragma unroll
@@ -1170,12 +1210,23 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
     xq = min(nr + TKY - 1, H - kyA) * W * xrowb / 16;
     const char* gs = (const char*)g + ((size_t)b0 * Ho + y0) * Wo * grow;
     const char* xs = (const char*)x + ((size_t)b0 * H + y0 + kyA) * W * xrowb;
-    FFMP_WGRAD_LOAD(gs, xs)
+    if constexpr (DMA) {
+      dma_stage(0, gs, xs, gq, xq);
+    } else {
+      FFMP_WGRAD_LOAD(gs, xs)
+    }
   }
   for (int st = 0; st < nstages; ++st) {
-    __syncthreads();  // the previous stage's reads are done
-    FFMP_WGRAD_STORE()
-    __syncthreads();
+    if constexpr (DMA) {
+      // stage st landed (the barrier's vmcnt(0)), and every wave is done with buffer (st + 1) & 1
+      __syncthreads();
+      gimg = lds + (st & 1) * SB;
+      ximg = gimg + (Pmax + KP) * grow;
+    } else {
+      __syncthreads();  // the previous stage's reads are done
+      FFMP_WGRAD_STORE()
+      __syncthreads();
+    }
     const int nr = min(R, Ho - (st % stages_per_sample) * R);
     if (st + 1 < nstages) {  // the next stage, in flight while this one is consumed
       const int b = b0 + (st + 1) / stages_per_sample, y0 = ((st + 1) % stages_per_sample) * R;
@@ -1184,7 +1235,11 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
       xq = min(nr1 + TKY - 1, H - y0 - kyA) * W * xrowb / 16;
       const char* gs = (const char*)g + ((size_t)b * Ho + y0) * Wo * grow;
       const char* xs = (const char*)x + ((size_t)b * H + y0 + kyA) * W * xrowb;
-      FFMP_WGRAD_LOAD(gs, xs)
+      if constexpr (DMA) {
+        dma_stage((st + 1) & 1, gs, xs, gq, xq);
+      } else {
+        FFMP_WGRAD_LOAD(gs, xs)
+      }
     }
     const int Ps = nr * Wo;
     // this lane's two k rows per k-step (u = 0, 1): position p = k0 + 8 fk + 4u + q, as (stage
@@ -1303,12 +1358,21 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
   // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
   const int ms = ffmp_detail::mfma_for(32) == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
+  // LDS-DMA staging into two stage buffers (FFMP_TUNE_CONV_WGDMA: 1, or 2 with the k-step prefetch):
+  // the 32x32x16 shape, stages of up to 8 rows in 2 x 80 KiB
+  const int wgdma = ms == 32 ? ffmp_detail::g_conv_wgdma : 0;
   int R = std::min(Ho, 8);
   auto bytes = [&](int rr) { return (size_t)(rr * Wo + kp) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
   auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };
-  while (R > 1 && (bytes(R) > 48 * 1024 || pieces(R) > kWgradPieces * 256)) --R;
-  if (bytes(R) > 64 * 1024 || pieces(R) > kWgradPieces * 256)
-    return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: rows of %d x %d x %d do not fit one stage", W, C, N);
+  if (wgdma) {
+    while (R > 1 && bytes(R) > 80 * 1024) --R;
+    if (bytes(R) > 80 * 1024)
+      return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: rows of %d x %d x %d do not fit one stage", W, C, N);
+  } else {
+    while (R > 1 && (bytes(R) > 48 * 1024 || pieces(R) > kWgradPieces * 256)) --R;
+    if (bytes(R) > 64 * 1024 || pieces(R) > kWgradPieces * 256)
+      return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: rows of %d x %d x %d do not fit one stage", W, C, N);
+  }
   if (Wo < 8) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: output rows of %d < 8 positions", Wo);
   const int per_chunk = (B + chunks - 1) / chunks;
   const dim3 grid((KH / TKY) * (KW / TKX), (B + per_chunk - 1) / per_chunk);
@@ -1319,7 +1383,14 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
                        per_chunk);
   };
   const bool pf = ffmp_detail::g_conv_wgpf != 0;
-  if (ms == 16) {
+  if (wgdma) {
+    if (wgdma == 2)
+      hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 32, true, true>), grid, dim3(256), 2 * bytes(R), s,
+                         (const __bf16*)g, (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+    else
+      hipLaunchKernelGGL((conv_wgrad_kernel<C, N, TW, 32, false, true>), grid, dim3(256), 2 * bytes(R), s,
+                         (const __bf16*)g, (const __bf16*)x, part, B, H, W, KH, KW, dx, TKY, TKX, R, per_chunk);
+  } else if (ms == 16) {
     if (pf) go(std::integral_constant<int, 16>{}, std::true_type{});
     else go(std::integral_constant<int, 16>{}, std::false_type{});
   } else {

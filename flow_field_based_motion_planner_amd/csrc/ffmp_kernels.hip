@@ -50,6 +50,7 @@ int conv_ba2_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_BA2)
 int conv_mbw_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_MBW)
 int conv_planar_swap(int v);         // ffmp_conv.hip (FFMP_TUNE_CONV_PLANAR)
 int conv_pin_swap(int v);            // ffmp_conv.hip (FFMP_TUNE_CONV_PIN)
+int conv_wgdma_swap(int v);          // ffmp_conv.hip (FFMP_TUNE_CONV_WGDMA)
 }  // namespace ffmp_detail
 using ffmp_detail::fail;
 using ffmp_detail::g_err;
@@ -1743,6 +1744,9 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
     case FFMP_TUNE_CONV_WGPF:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "weight-gradient prefetch must be 0 or 1");
       return ffmp_detail::conv_wgpf_swap(value);
+    case FFMP_TUNE_CONV_WGDMA:
+      if (value < 0 || value > 2) return fail(FFMP_E_ARG, "conv weight-gradient DMA must be 0-2");
+      return ffmp_detail::conv_wgdma_swap(value);
     case FFMP_TUNE_CONV_PIN:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv pinned schedule must be 0 or 1");
       return ffmp_detail::conv_pin_swap(value);

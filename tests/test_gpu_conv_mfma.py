@@ -336,3 +336,29 @@ def test_dgrad_and_wgrad_mfma_shapes_match_float64(conv_knobs, mfma):
             rw = torch.nn.grad.conv2d_weight(x64, (N, C, KH, KW), gy64, dilation=(1, d)).permute(2, 3, 0, 1)
             aw = torch.nn.grad.conv2d_weight(x64.abs(), (N, C, KH, KW), gy64.abs(), dilation=(1, d)).permute(2, 3, 0, 1)
         assert not bool(((dw.double() - rw).abs() > 5e-5 * aw + 1e-6).any()), (mfma, B, H, KH)
+
+
+@pytest.mark.parametrize("wgdma", [1, 2])
+def test_wgrad_dma_stages_match_float64(wgdma):
+    """The weight gradient with LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA 1, 2 = with the
+    k-step prefetch) against float64: conv2's shape (64-channel g rows swizzled), conv3's (64-channel x
+    rows swizzled too), the folded conv1's and a ragged one (partial last stage, batch chunks)."""
+    from flow_field_based_motion_planner_amd import _abi
+    from flow_field_based_motion_planner_amd.conv_mfma import conv2d_wgrad_nhwc
+    lib = _abi.load()
+    prev = lib.ffmp_set_tuning(_abi.TUNE_CONV_WGDMA, wgdma)
+    try:
+        g0 = torch.Generator(device=DEV).manual_seed(100 + wgdma)
+        for (B, H, W, C, KH, KW, N, d) in [(3, 69, 69, 32, 32, 32, 64, 1), (3, 38, 38, 64, 8, 8, 64, 1),
+                                           (2, 100, 85, 32, 32, 2, 32, 16), (5, 20, 22, 32, 6, 4, 32, 1)]:
+            x = torch.randn((B, H, W, C), device=DEV, generator=g0).to(torch.bfloat16)
+            gy = torch.randn((B, H - KH + 1, W - (KW - 1) * d, N), device=DEV, generator=g0).to(torch.bfloat16)
+            dw = conv2d_wgrad_nhwc(gy, x, KH, KW, dx=d, chunks=2)
+            x64, gy64 = x.double().permute(0, 3, 1, 2), gy.double().permute(0, 3, 1, 2)
+            with torch.backends.cudnn.flags(enabled=False):
+                rw = torch.nn.grad.conv2d_weight(x64, (N, C, KH, KW), gy64, dilation=(1, d)).permute(2, 3, 0, 1)
+                aw = torch.nn.grad.conv2d_weight(x64.abs(), (N, C, KH, KW), gy64.abs(), dilation=(1, d)).permute(2, 3, 0, 1)
+            bad = (dw.double() - rw).abs() > 5e-5 * aw + 1e-6
+            assert not bool(bad.any()), (wgdma, B, H, C, KH, N, int(bad.sum()))
+    finally:
+        lib.ffmp_set_tuning(_abi.TUNE_CONV_WGDMA, prev)

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """A/B of the convolution kernels' launch variants — the MFMA shape (FFMP_TUNE_CONV_MFMA: 16 = 16x16x32,
 32 = 32x32x16) and the kernel rows per ring step of the row-ring forward (FFMP_TUNE_CONV_KYS: 0 = by shape,
-1, 2, 4) the B operand through LDS (FFMP_TUNE_CONV_LB), the weight gradient's operand prefetch (FFMP_TUNE_CONV_WGPF), B two taps ahead (FFMP_TUNE_CONV_BA2) the forward's position blocks per wave (FFMP_TUNE_CONV_MBW) its planar slots (FFMP_TUNE_CONV_PLANAR) and pinned schedule (FFMP_TUNE_CONV_PIN) — on the reference Network's layers at batch B (default 256), random data, interleaved rounds in
+1, 2, 4) the B operand through LDS (FFMP_TUNE_CONV_LB), the weight gradient's operand prefetch (FFMP_TUNE_CONV_WGPF), B two taps ahead (FFMP_TUNE_CONV_BA2) the forward's position blocks per wave (FFMP_TUNE_CONV_MBW) its planar slots (FFMP_TUNE_CONV_PLANAR) pinned schedule (FFMP_TUNE_CONV_PIN) and the weight gradient's LDS-DMA stages (FFMP_TUNE_CONV_WGDMA) — on the reference Network's layers at batch B (default 256), random data, interleaved rounds in
 ONE process (cdna_hip_programming.md rule 24): per layer and variant the median / min ms and PF/s over
 the rounds, and each variant's max error against a float64 convolution of the same bf16 operands (first
-4 samples).  Usage: python tools/conv_ab.py [B] [rounds] [variant ...]   (variant = mfma:kys:lb:wgpf:ba2:mbw:planar:pin, e.g. 32:1:0:0:0:3:0:1)"""
+4 samples).  Usage: python tools/conv_ab.py [B] [rounds] [variant ...]   (variant = mfma:kys:lb:wgpf:ba2:mbw:planar:pin:wgdma, e.g. 32:1:0:0:0:3:0:0:1)"""
 import os
 import sys
 
@@ -20,8 +20,8 @@ from flow_field_based_motion_planner_amd.conv_mfma import (conv2d_dgrad_nhwc, co
 dev = torch.device("cuda:0")
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-VARIANTS = [tuple(int(v) for v in (a + ":0:0:0:0:0:0:0").split(":")[:8]) for a in sys.argv[3:]] or \
-    [(0, 0, 0, 0, 0, 0, 0, 0), (0, 0, 0, 0, 0, 0, 0, 1)]
+VARIANTS = [tuple(int(v) for v in (a + ":0:0:0:0:0:0:0:0").split(":")[:9]) for a in sys.argv[3:]] or \
+    [(0, 0, 0, 0, 0, 0, 0, 0, 0), (0, 0, 0, 0, 0, 0, 0, 0, 1)]
 torch.manual_seed(0)
 
 
@@ -56,6 +56,10 @@ layers["conv2 dgrad_bm"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32, lambda: conv2
                                 g2[:4].permute(0, 3, 1, 2).double(), x2[:4].permute(0, 3, 1, 2).double(), w2.double(),
                                 None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0])
 layers["conv2 wgrad"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32, lambda: conv2d_wgrad_nhwc(g2, x2, 32, 32), None)
+# conv3's weight gradient (64 -> 64, k 8, 38^2 -> 31^2)
+g3 = rnd(B, 31, 31, 64)
+x3w = torch.relu(rnd(B, 38, 38, 64))
+layers["conv3 wgrad"] = (2.0 * B * 31 * 31 * 64 * 64 * 64, lambda: conv2d_wgrad_nhwc(g3, x3w, 8, 8), None)
 # conv1: 2 -> 32, k 32, 100^2 -> 69^2, folded (F = 16), bf16 out + ReLU
 x1 = torch.rand(B, 2, 100, 100, device=dev) * 255
 w1 = rnd(32, 2, 32, 32, scale=1 / 45.0)
@@ -83,6 +87,7 @@ def setv(v):
     lib.ffmp_set_tuning(_abi.TUNE_CONV_MBW, v[5])
     lib.ffmp_set_tuning(_abi.TUNE_CONV_PLANAR, v[6])
     lib.ffmp_set_tuning(_abi.TUNE_CONV_PIN, v[7])
+    lib.ffmp_set_tuning(_abi.TUNE_CONV_WGDMA, v[8])
 
 
 res = {k: {s: [] for s in VARIANTS} for k in layers}
@@ -103,7 +108,7 @@ for rnd_i in range(ROUNDS):
         setv(s)
         for k, (flop, fn, ref) in layers.items():
             res[k][s].append(timeit(fn))
-setv((0, 0, 0, 0, 0, 0, 0, 0))
+setv((0, 0, 0, 0, 0, 0, 0, 0, 0))
 for k, (flop, fn, ref) in layers.items():
     line = [f"{k:20s} B={B}"]
     for s in VARIANTS:

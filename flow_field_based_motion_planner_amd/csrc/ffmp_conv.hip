@@ -79,8 +79,8 @@ int conv_pin_swap(int v) {
   g_conv_pin = v;
   return prev;
 }
-// the weight gradient's LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA): 0 = off, 1 = on, 2 = on with
-// the k-step prefetch
+// the weight gradient's LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA): 0 = by shape (with the k-step
+// prefetch where the kernel runs one workgroup per CU), 1 = on, 2 = on with the prefetch, 3 = off
 int g_conv_wgdma = 0;
 int conv_wgdma_swap(int v) {
   const int prev = g_conv_wgdma;
@@ -1358,9 +1358,16 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
   // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
   const int ms = ffmp_detail::mfma_for(32) == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
-  // LDS-DMA staging into two stage buffers (FFMP_TUNE_CONV_WGDMA: 1, or 2 with the k-step prefetch):
-  // the 32x32x16 shape, stages of up to 8 rows in 2 x 80 KiB
-  const int wgdma = ms == 32 ? ffmp_detail::g_conv_wgdma : 0;
+  // LDS-DMA staging into two stage buffers with the k-step prefetch (FFMP_TUNE_CONV_WGDMA), the 32x32x16
+  // shape, stages of up to 8 rows in 2 x 80 KiB.  Default: where the kernel holds one workgroup per CU
+  // anyway (more than 8 accumulator blocks per wave: conv2's 32 -> 64, 1.70 -> 1.47 ms at B = 256,
+  // 6.69 -> 5.75 ms at 1,024); the 2 x 80 KiB would cost the smaller ones their second and third
+  // workgroup per CU (conv3's 64 -> 64: 0.180 -> 0.242 ms; profiles/r06e_conv_ab_wgdma.txt)
+  int wgdma = 0;
+  if (ms == 32) {
+    const int knob = ffmp_detail::g_conv_wgdma;
+    wgdma = knob == 3 ? 0 : knob != 0 ? knob : (TW * (N / 32) * (C / 32) > 8 ? 2 : 0);
+  }
   int R = std::min(Ho, 8);
   auto bytes = [&](int rr) { return (size_t)(rr * Wo + kp) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
   auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };

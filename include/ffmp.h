@@ -209,7 +209,8 @@ int64_t ffmp_layout(int32_t which);
 #define FFMP_TUNE_CONV_PIN 14   /* 1: the row-ring forward's default launch with each half-trip's loads pinned ahead
                                    of its MFMAs by scheduling barriers; 0 (default): the compiler's schedule */
 #define FFMP_TUNE_CONV_WGDMA 15 /* the weight gradient's stages copied by LDS-DMA into two LDS buffers (one barrier
-                                   per stage): 1 = on, 2 = on with the k-step operand prefetch; 0 (default): off */
+                                   per stage): 0 (default) = with the k-step prefetch where the kernel runs one
+                                   workgroup per CU (32 -> 64 channels), 1 = on, 2 = on with the prefetch, 3 = off */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

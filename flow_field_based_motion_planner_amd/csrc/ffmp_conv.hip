@@ -1243,14 +1243,17 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
     }
     const int Ps = nr * Wo;
     // this lane's two k rows per k-step (u = 0, 1): position p = k0 + 8 fk + 4u + q, as (stage
-    // row, column), advanced by KP per k-step without branches on data (Wo >= 8: host check)
-    int pr[2], pc[2];
+    // row, column), advanced by KP per k-step without branches on data (Wo >= 8: host check); xo = the
+    // byte offset of its x image row (pr W + pc) xrowb, advanced with it (no multiply per k-step)
+    int pr[2], pc[2], xo[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = 8 * fk + 4 * u + q;
       pr[u] = p / Wo;
       pc[u] = p - pr[u] * Wo;
+      xo[u] = (pr[u] * W + pc[u]) * xrowb;
     }
+    const int xwrap = (W - Wo) * xrowb;  // x bytes skipped when a position row wraps
     // each operand fragment = two transposing reads (k rows 8 fk + 4u .. +4), joined as whole
     // vectors (element-wise assembly of the 4 x 16-bit results miscompiles: ROCm 7.2)
     auto fetch = [&](int k0, s16x4 (&ar)[AN][2], s16x4 (&br)[TW][AC][2]) {
@@ -1265,7 +1268,7 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
           const int off = N == 64 ? ((col & ~15) ^ swz128(grw)) | (col & 15) : col;
           ar[nb][u] = tr_read(gimg + grw * grow + off);
         }
-        const int base = in ? pr[u] * W + pc[u] : 0;
+        const int base = in ? pr[u] * W + pc[u] : 0;  // (C = 64: xo in C = 32's form below)
         if constexpr (C == 64) {  // 128-byte rows: the chunk swizzle depends on each read's row
 #pragma unroll
           for (int t = 0; t < TW; ++t) {
@@ -1277,18 +1280,18 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
             }
           }
         } else {  // one lane address per k row, plus a scalar tap offset and a constant column offset
-          const char* xl = ximg + base * xrowb + acol0;
+          const char* xl = ximg + (in ? xo[u] : 0) + acol0;
 #pragma unroll
           for (int t = 0; t < TW; ++t)
 #pragma unroll
             for (int cb = 0; cb < AC; ++cb) br[t][cb][u] = tr_read(xl + toff[t] + cb * MS * 2);
         }
-        int c = pc[u] + KP, rr = pr[u];
-#pragma unroll
-        for (int wrap = 0; wrap < KP / 8; ++wrap)
-          if (c >= Wo) c -= Wo, ++rr;
+        int c = pc[u] + KP, rr = pr[u], xr = xo[u] + KP * xrowb;
+        if (c >= Wo) c -= Wo, ++rr, xr += xwrap;
+        if (Wo < KP && c >= Wo) c -= Wo, ++rr, xr += xwrap;  // (a second wrap only for rows under KP)
         pc[u] = c;
         pr[u] = rr;
+        xo[u] = xr;
       }
     };
     auto mma = [&](const s16x4 (&ar)[AN][2], const s16x4 (&br)[TW][AC][2]) {

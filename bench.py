@@ -442,6 +442,17 @@ def run_leg(args, name, cfg, n, offset, K, W, dev, world, rank, strong, main_leg
             graph_rem.replay(actions[:rem])
             for k in range(rem, per):
                 env.step(actions[k])
+        # The graph warm-ups and the skew trial above stepped every env ~150-190 steps past the warm-up.
+        # Every env starts its first episode at the same reset, so the ~85 % that survive max_steps (200)
+        # random-action steps truncate and reset on the SAME step. After the 8-round skew trial that step
+        # fell inside the 20 timed steps: 27,807 resets in the window against 611 (profiles/r06g_*,
+        # r06h_*), 13.4-13.7 vs 13.9-14.0 M. A long run pays that step once per 200. Restart the episodes
+        # instead: reset, then the W warm-up steps again, which also brings the ring back to the position
+        # the graphs were captured at. The timed steps then start from a fresh reset plus warm-up, as
+        # they did before the trials existed.
+        env.reset()
+        for w in range(W):
+            env.step(actions[w])
         # re-warm: the captures above (torch.cuda.graph synchronizes, collects garbage and empties the
         # cache) leave the GPU idle for a while, and after an idle gap the first few ms of steps run slow
         # (profiles/r03b_transient*.txt) — at the 8-GPU strong leg's 0.6-ms steps the driver's 20 timed

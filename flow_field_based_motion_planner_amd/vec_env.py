@@ -556,11 +556,13 @@ class FFMPVec:
     # slow slot/potential pairings; the step loop itself is the judge: time every slot's
     # newest-only raster over two ring cycles (after SLOT_WARMUP_CYCLES untimed ones) and rebuild
     # the ring with new pieces for slots more than SLOW_SLOT above the fastest (ffmp_ring_rebuild),
-    # up to REPAIR_ROUNDS times, keeping the rebuilt ring only if its cycle is faster.  (The 12 %
-    # threshold of rounds 1-3 guarded against rebuilds judged on post-idle timings; with the
-    # warm-up, 6 %: profiles/r04h_slot_repair.txt.)
+    # up to REPAIR_ROUNDS times, keeping the rebuilt ring only if its cycle is faster; a reverted
+    # rebuild does not end the repair — the next round draws other pieces (round 6: one C3 box kept a
+    # slot 15 % slow after its single rebuild came out worse, 13.41 vs 13.71 M on the same box,
+    # profiles/r06g_bench_default_*.json).  (The 12 % threshold of rounds 1-3 guarded against rebuilds
+    # judged on post-idle timings; with the warm-up, 6 %: profiles/r04h_slot_repair.txt.)
     SLOW_SLOT = 1.06
-    REPAIR_ROUNDS = 2
+    REPAIR_ROUNDS = 3
     PAIR_SLOTS = True  # build the ring's slots from pieces probed against the potential plane
 
     # untimed ring cycles before the slot timing: the timing follows host work (construction, a
@@ -698,15 +700,16 @@ class FFMPVec:
                 torch.cuda.synchronize(self.device)
                 self._ring.drop_previous()
                 ms = new
-            else:  # the rebuilt ring cycles slower: back to the previous one, stop repairing
+            else:  # the rebuilt ring cycles slower: back to the previous one, then another round
                 history.append({"slot_ms": [round(new[i], 3) for i in sorted(new)], "reverted": True})
                 torch.cuda.synchronize(self.device)
                 self._ring.revert()
                 self._adopt_ring_tensor()
                 self._clear_after_tuning()
-                break
-        else:
-            history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)], "slow": []})
+        else:  # every round rebuilt: the kept ring's timing (slots still slow if the last rebuilds lost)
+            fast = min(ms.values())
+            history.append({"slot_ms": [round(ms[i], 3) for i in sorted(ms)],
+                            "slow": [i for i, v in ms.items() if v > self.SLOW_SLOT * fast]})
         self.ring_meta = dict(self.ring_meta or {}, **self._ring.info(), repair=history)
 
     def tuning(self) -> dict:

@@ -60,6 +60,14 @@ layers["conv2 wgrad"] = (2.0 * B * 38 * 38 * 64 * 32 * 32 * 32, lambda: conv2d_w
 g3 = rnd(B, 31, 31, 64)
 x3w = torch.relu(rnd(B, 38, 38, 64))
 layers["conv3 wgrad"] = (2.0 * B * 31 * 31 * 64 * 64 * 64, lambda: conv2d_wgrad_nhwc(g3, x3w, 8, 8), None)
+# the folded conv1's weight gradient (32 folded channels, 32 x 2 taps at dx 16, 69^2 positions)
+g1 = rnd(B, 69, 69, 32)
+x1w = rnd(B, 100, 85, 32)
+layers["conv1 wgrad (fold)"] = (2.0 * B * 69 * 69 * 32 * 32 * 32 * 2, lambda: conv2d_wgrad_nhwc(g1, x1w, 32, 2, dx=16), None)
+# conv4's weight gradient (64 -> 64, k 8, 31^2 -> 24^2)
+g4 = rnd(B, 24, 24, 64)
+x4w = torch.relu(rnd(B, 31, 31, 64))
+layers["conv4 wgrad"] = (2.0 * B * 24 * 24 * 64 * 64 * 64, lambda: conv2d_wgrad_nhwc(g4, x4w, 8, 8), None)
 # conv1: 2 -> 32, k 32, 100^2 -> 69^2, folded (F = 16), bf16 out + ReLU
 x1 = torch.rand(B, 2, 100, 100, device=dev) * 255
 w1 = rnd(32, 2, 32, 32, scale=1 / 45.0)

@@ -5,5 +5,5 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r06j
 mkdir -p $O
 cd $R
-timeout -k 10 400 python -u tools/conv_ab.py 256 7 0 16:1 16:1:0:0:0:2 16:1:0:0:0:4 32:1:0:0:0:2 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
+timeout -k 10 400 python -u tools/conv_ab.py 256 7 0 16 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
 cat $O/conv_ab.txt

@@ -38,9 +38,10 @@ int fail(int code, const char* fmt, ...);  // ffmp_kernels.hip (sets ffmp_last_e
 // ffmp_conv2d_check: run every shape check of a launch, then return before launching
 thread_local bool t_conv_dry = false;
 // the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 0 = each kernel's
-// default (32x32x16 everywhere: profiles/r06a_conv_ab.txt, r06b_conv_ab.txt — the 16x16x32 stream ran
-// 6-50 % slower on the forwards and the weight gradient, and the samples-as-M data gradient within
-// the run-to-run spread of 32x32x16), 16 = 16x16x32, 32 = 32x32x16
+// default (32x32x16 for the forwards, the data gradient and conv2's weight gradient: profiles/r06a_conv_ab.txt,
+// r06b_conv_ab.txt — the 16x16x32 stream ran 6-50 % slower there, the samples-as-M data gradient within
+// the run-to-run spread; 16x16x32 for the other weight gradients, 6-15 % faster:
+// profiles/r06j_conv_ab_wgrad_ms16.txt), 16 = 16x16x32, 32 = 32x32x16
 int g_conv_mfma = 0;
 int mfma_for(int dflt) { return g_conv_mfma ? g_conv_mfma : dflt; }
 int conv_mfma_swap(int v) {
@@ -1360,7 +1361,11 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   const int TKX = std::min(KW, TG), TKY = TG / TKX;
   if (KW % TKX || KH % TKY) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: kernel %d x %d does not tile by %d taps", KH, KW, TG);
   // stage rows R: the most rows whose g + x images fit 48 KiB of LDS and 12 register pieces
-  const int ms = ffmp_detail::mfma_for(32) == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
+  // MFMA shape: 16x16x32 by default except for the 32 -> 64 layer (conv2: 1.35 vs 1.66 ms on 16x16x32, and
+  // its LDS-DMA stages below are built for 32x32x16); the other layers' weight gradients ran faster on it
+  // (conv1 folded 0.415 -> 0.352 ms, conv3 0.186 -> 0.162, conv4 0.118 -> 0.111 at B = 256;
+  // profiles/r06j_conv_ab_wgrad_ms16.txt)
+  const int ms = ffmp_detail::mfma_for(C == 32 && N == 64 ? 32 : 16) == 16 ? 16 : 32, kp = ms == 16 ? 32 : 16;  // + kp zero g rows
   // LDS-DMA staging into two stage buffers with the k-step prefetch (FFMP_TUNE_CONV_WGDMA), the 32x32x16
   // shape, stages of up to 8 rows in 2 x 80 KiB.  Default: where the kernel holds one workgroup per CU
   // anyway (more than 8 accumulator blocks per wave: conv2's 32 -> 64, 1.70 -> 1.47 ms at B = 256,

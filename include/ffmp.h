@@ -190,9 +190,11 @@ int64_t ffmp_layout(int32_t which);
                                    ones the ring needs (pairing candidates; they stay pooled):
                                    0 = default (need/2 + 4), v >= 1 = at most v - 1.  An HBM
                                    budget (FFMPVec hbm_budget) sets it around its ring creation. */
-#define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 0 (default:
-                                   32x32x16, measured fastest), 16 (v_mfma_f32_16x16x32_bf16) or 32
-                                   (v_mfma_f32_32x32x16_bf16); the same products, fp32 sums in another order */
+#define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 0 (default, each
+                                   kernel's measured fastest: 32x32x16 for the forwards, the data gradient and
+                                   the 32 -> 64 weight gradient, 16x16x32 for the other weight gradients), 16
+                                   (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); the same
+                                   products, fp32 sums in another order */
 #define FFMP_TUNE_CONV_KYS 8    /* kernel rows per ring step of the row-ring convolution forward: 0 (default,
                                    1), 1, 2 or 4 (the same products and sums) */
 #define FFMP_TUNE_CONV_LB 9     /* 1: the unpadded row-ring forward shares each tap's weights through LDS

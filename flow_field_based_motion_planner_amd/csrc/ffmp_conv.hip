@@ -1289,7 +1289,11 @@ __global__ __launch_bounds__(256, (TW * (N / 32) * (C / 32) > 8 ? 1 : 2)) void c
         }
         int c = pc[u] + KP, rr = pr[u], xr = xo[u] + KP * xrowb;
         if (c >= Wo) c -= Wo, ++rr, xr += xwrap;
-        if (Wo < KP && c >= Wo) c -= Wo, ++rr, xr += xwrap;  // (a second wrap only for rows under KP)
+        if (Wo < KP) {  // rows shorter than a k-step: up to KP / 8 wraps in all (Wo >= 8: host check)
+#pragma unroll
+          for (int wrap = 1; wrap < KP / 8; ++wrap)
+            if (c >= Wo) c -= Wo, ++rr, xr += xwrap;
+        }
         pc[u] = c;
         pr[u] = rr;
         xo[u] = xr;

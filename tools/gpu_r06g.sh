@@ -10,7 +10,7 @@ tail -3 $O/pytest_gpu.log; grep -E "^FAILED" $O/pytest_gpu.log | head
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-for rep in 1 2; do
+for rep in 1; do
   timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_default_$rep.json 2> $O/bench_default_$rep.err || { tail -20 $O/bench_default_$rep.err; exit 1; }
   python -c "import json; d=json.loads(open('$O/bench_default_$rep.json').read().strip().splitlines()[-1]); print('default', round(d['value']/1e6,3), round(d['roofline']['frac'],4), round(d['hbm_roofline_pct_whole_step'],2), d['cpu_baseline']['value'] if d.get('cpu_baseline') else None)"
 done

@@ -967,6 +967,15 @@ int launch_fwd_mbw(const void* x, const void* w, const float* bias, void* y, int
         return;
       }
     }
+    // one channel block, several kernel rows per ring step (FFMP_TUNE_CONV_KYS 2 / 4): the next rows in
+    // 2 registers per thread where they fit (rows up to 8 KiB: the folded conv1's 5.3 KiB)
+    if constexpr (NB == 1 && !PAD && kMS == 32 && kKYS > 1) {
+      if (chunks <= 512) {
+        hipLaunchKernelGGL((conv_fwd_kernel<C, NB, MBW, PAD, WF, 32, kKYS, 2>), grid, dim3(256), lds, s,
+                           (const __bf16*)x, (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, ring, flags);
+        return;
+      }
+    }
     // conv2's shape (32 -> 64, unpadded): the pinned-schedule variants (FFMP_TUNE_CONV_BA2: 1 = B two
     // taps ahead with rows in 2 registers where the row fits, 2 = B one tap ahead)
     if constexpr (C == 32 && NB == 2 && !PAD && kMS == 32 && kKYS == 1) {

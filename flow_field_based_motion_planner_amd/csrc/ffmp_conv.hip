@@ -81,7 +81,8 @@ int conv_pin_swap(int v) {
   return prev;
 }
 // the weight gradient's LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA): 0 = by shape (with the k-step
-// prefetch where the kernel runs one workgroup per CU), 1 = on, 2 = on with the prefetch, 3 = off
+// prefetch where the kernel runs one workgroup per CU), 1 = on, 2 = on with the prefetch, 3 = off, 4 = the
+// 32 -> 64 layer with 4 taps per wave (two workgroups per CU) on prefetched LDS-DMA stages
 int g_conv_wgdma = 0;
 int conv_wgdma_swap(int v) {
   const int prev = g_conv_wgdma;
@@ -1387,14 +1388,17 @@ int launch_wgrad(const void* g, const void* x, float* part, int B, int H, int W,
   int wgdma = 0;
   if (ms == 32) {
     const int knob = ffmp_detail::g_conv_wgdma;
-    wgdma = knob == 3 ? 0 : knob != 0 ? knob : (TW * (N / 32) * (C / 32) > 8 ? 2 : 0);
+    wgdma = knob == 3 ? 0 : knob == 4 ? 2 : knob != 0 ? knob : (TW * (N / 32) * (C / 32) > 8 ? 2 : 0);
   }
+  // two stage buffers per workgroup: 2 x 80 KiB where the kernel holds one workgroup per CU anyway,
+  // 2 x 40 KiB (two workgroups per CU) otherwise
+  const size_t stage_cap = TW * (N / 32) * (C / 32) > 8 ? 80 * 1024 : 40 * 1024;
   int R = std::min(Ho, 8);
   auto bytes = [&](int rr) { return (size_t)(rr * Wo + kp) * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2; };
   auto pieces = [&](int rr) { return ((size_t)rr * Wo * N * 2 + (size_t)(rr + TKY - 1) * W * C * 2) / 16; };
   if (wgdma) {
-    while (R > 1 && bytes(R) > 80 * 1024) --R;
-    if (bytes(R) > 80 * 1024)
+    while (R > 1 && bytes(R) > stage_cap) --R;
+    if (bytes(R) > stage_cap)
       return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad: rows of %d x %d x %d do not fit one stage", W, C, N);
   } else {
     while (R > 1 && (bytes(R) > 48 * 1024 || pieces(R) > kWgradPieces * 256)) --R;
@@ -1662,7 +1666,10 @@ int ffmp_conv2d_wgrad_bf16(const void* g, const void* x, float* part, int32_t ba
                 batch, h, wd, kh, kw, dx, chunks);
   if (((uintptr_t)g | (uintptr_t)x) & 15) return fail(FFMP_E_ARG, "ffmp_conv2d_wgrad_bf16: g and x must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  if (c == 32 && n == 64) return launch_wgrad<32, 64, FFMP_WGRAD_TW_3264>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  if (c == 32 && n == 64) {  // FFMP_TUNE_CONV_WGDMA 4: 4 taps per wave, LDS-DMA stages, two workgroups per CU
+    if (ffmp_detail::g_conv_wgdma == 4) return launch_wgrad<32, 64, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+    return launch_wgrad<32, 64, FFMP_WGRAD_TW_3264>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
+  }
   if (c == 64 && n == 64) return launch_wgrad<64, 64, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 32 && n == 32) return launch_wgrad<32, 32, 2>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);
   if (c == 64 && n == 32) return launch_wgrad<64, 32, 4>(g, x, part, batch, h, wd, kh, kw, dx, chunks, s);

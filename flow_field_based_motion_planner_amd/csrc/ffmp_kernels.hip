@@ -1745,7 +1745,7 @@ int32_t ffmp_set_tuning(int32_t key, int32_t value) {
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "weight-gradient prefetch must be 0 or 1");
       return ffmp_detail::conv_wgpf_swap(value);
     case FFMP_TUNE_CONV_WGDMA:
-      if (value < 0 || value > 3) return fail(FFMP_E_ARG, "conv weight-gradient DMA must be 0-3");
+      if (value < 0 || value > 4) return fail(FFMP_E_ARG, "conv weight-gradient DMA must be 0-4");
       return ffmp_detail::conv_wgdma_swap(value);
     case FFMP_TUNE_CONV_PIN:
       if (value != 0 && value != 1) return fail(FFMP_E_ARG, "conv pinned schedule must be 0 or 1");

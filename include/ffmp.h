@@ -212,7 +212,8 @@ int64_t ffmp_layout(int32_t which);
                                    of its MFMAs by scheduling barriers; 0 (default): the compiler's schedule */
 #define FFMP_TUNE_CONV_WGDMA 15 /* the weight gradient's stages copied by LDS-DMA into two LDS buffers (one barrier
                                    per stage): 0 (default) = with the k-step prefetch where the kernel runs one
-                                   workgroup per CU (32 -> 64 channels), 1 = on, 2 = on with the prefetch, 3 = off */
+                                   workgroup per CU (32 -> 64 channels), 1 = on, 2 = on with the prefetch, 3 = off,
+                                   4 = the 32 -> 64 layer with 4 taps per wave, two workgroups per CU */
 int32_t ffmp_set_tuning(int32_t key, int32_t value);
 
 /* Host-side, float64: the footprint of ffmp.py:87-94 generalised to G

@@ -338,10 +338,10 @@ def test_dgrad_and_wgrad_mfma_shapes_match_float64(conv_knobs, mfma):
         assert not bool(((dw.double() - rw).abs() > 5e-5 * aw + 1e-6).any()), (mfma, B, H, KH)
 
 
-@pytest.mark.parametrize("wgdma", [1, 2, 3])
+@pytest.mark.parametrize("wgdma", [1, 2, 3, 4])
 def test_wgrad_dma_stages_match_float64(wgdma):
     """The weight gradient with LDS-DMA double-buffered stages (FFMP_TUNE_CONV_WGDMA 1, 2 = with the
-    k-step prefetch) and without them (3) against float64: conv2's shape (64-channel g rows swizzled), conv3's (64-channel x
+    k-step prefetch, 4 = conv2's shape at 4 taps per wave) and without them (3) against float64: conv2's shape (64-channel g rows swizzled), conv3's (64-channel x
     rows swizzled too), the folded conv1's and a ragged one (partial last stage, batch chunks)."""
     from flow_field_based_motion_planner_amd import _abi
     from flow_field_based_motion_planner_amd.conv_mfma import conv2d_wgrad_nhwc

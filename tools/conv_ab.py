@@ -76,6 +76,16 @@ wf1 = frag_order(pack_weight_fold(w1, 16))
 layers["conv1 fwd (fold)"] = (2.0 * B * 69 * 69 * 32 * 2 * 32 * 32,
                               lambda: conv2d_nhwc(nhwc_bf16(x1), wf1, b1, relu=True, out_dtype=torch.bfloat16, dx=16,
                                                   x_fold=True), None)
+# conv3's and conv4's data gradients (the small-image kernel with implicit padding k - 1)
+from flow_field_based_motion_planner_amd.conv_mfma import pack_weight_dgrad  # noqa: E402
+w3d = rnd(64, 64, 8, 8, scale=1 / 22.6)
+wd3 = frag_order(pack_weight_dgrad(w3d))
+gd3 = rnd(B, 31, 31, 64)
+layers["conv3 dgrad (small)"] = (2.0 * B * 31 * 31 * 64 * 64 * 64, lambda: conv2d_nhwc(gd3, wd3, None, pad=7,
+                                                                                       out_dtype=torch.bfloat16), None)
+gd4 = rnd(B, 24, 24, 64)
+layers["conv4 dgrad (small)"] = (2.0 * B * 24 * 24 * 64 * 64 * 64, lambda: conv2d_nhwc(gd4, wd3, None, pad=7,
+                                                                                       out_dtype=torch.bfloat16), None)
 # conv3: 64 -> 64, k 8, 38^2 -> 31^2 (small-image kernel, fragment-order weights)
 x3 = torch.relu(rnd(B, 38, 38, 64))
 w3 = rnd(64, 64, 8, 8, scale=1 / 22.6)

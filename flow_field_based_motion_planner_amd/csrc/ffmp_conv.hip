@@ -40,8 +40,8 @@ thread_local bool t_conv_dry = false;
 // the MFMA shape of the convolution kernels that have both (FFMP_TUNE_CONV_MFMA): 0 = each kernel's
 // default (32x32x16 for the forwards, the data gradient and conv2's weight gradient: profiles/r06a_conv_ab.txt,
 // r06b_conv_ab.txt — the 16x16x32 stream ran 6-50 % slower there, the samples-as-M data gradient within
-// the run-to-run spread; 16x16x32 for the other weight gradients, 6-15 % faster:
-// profiles/r06j_conv_ab_wgrad_ms16.txt), 16 = 16x16x32, 32 = 32x32x16
+// the run-to-run spread; 16x16x32 for the other weight gradients, 6-15 % faster, and the small-image
+// kernel's padded data gradients, 3-6 %: profiles/r06j_conv_ab_*_ms16.txt), 16 = 16x16x32, 32 = 32x32x16
 int g_conv_mfma = 0;
 int mfma_for(int dflt) { return g_conv_mfma ? g_conv_mfma : dflt; }
 int conv_mfma_swap(int v) {
@@ -819,7 +819,9 @@ int launch_small(const void* x, const void* w, const float* bias, void* y, int B
   const size_t lds = std::max(small_window_bytes(Wo, KH, W, C), kSmallRedBytes);
   const dim3 grid((Ho * Wo + 127) / 128, B);
   if (t_conv_dry) return FFMP_OK;
-  if (ffmp_detail::mfma_for(32) == 16)
+  // MFMA shape: 16x16x32 for the padded (data-gradient) form — conv3's 0.199 -> 0.192 ms, conv4's 0.145 ->
+  // 0.137 at B = 256 — 32x32x16 for the forwards (conv3 0.153 vs 0.162; profiles/r06j_conv_ab_small_ms16.txt)
+  if (ffmp_detail::mfma_for(PAD ? 16 : 32) == 16)
     hipLaunchKernelGGL((conv_small_kernel<C, NB, PAD, WF, 16>), grid, dim3(256), lds, s, (const __bf16*)x,
                        (const __bf16*)w, bias, y, H, W, KH, KW, pad, dx, flags);
   else

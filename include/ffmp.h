@@ -192,7 +192,8 @@ int64_t ffmp_layout(int32_t which);
                                    budget (FFMPVec hbm_budget) sets it around its ring creation. */
 #define FFMP_TUNE_CONV_MFMA 7   /* MFMA shape of the convolution kernels that have both: 0 (default, each
                                    kernel's measured fastest: 32x32x16 for the forwards, the data gradient and
-                                   the 32 -> 64 weight gradient, 16x16x32 for the other weight gradients), 16
+                                   the 32 -> 64 weight gradient, 16x16x32 for the other weight gradients and
+                                   the small-image padded data gradients), 16
                                    (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); the same
                                    products, fp32 sums in another order */
 #define FFMP_TUNE_CONV_KYS 8    /* kernel rows per ring step of the row-ring convolution forward: 0 (default,

@@ -5,6 +5,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r06j
 mkdir -p $O
 cd $R
-timeout -k 10 400 python -u tools/conv_ab.py 256 9 0 16 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
+timeout -k 10 400 python -u tools/conv_ab.py 256 9 0 32 > $O/conv_ab.txt 2>&1 || { tail -20 $O/conv_ab.txt; exit 1; }
 cat $O/conv_ab.txt
-timeout -k 10 300 python -u -m pytest tests/test_gpu_conv_mfma.py -q -m gpu --timeout 200 --timeout-method thread -k "variants or wgrad" 2>&1 | tail -2
+timeout -k 10 300 python -u -m pytest tests/test_gpu_conv_mfma.py -q -m gpu --timeout 200 --timeout-method thread  2>&1 | tail -2
